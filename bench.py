@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Benchmark of the aggregation hot path (driver contract: one JSON line).
+
+Metric (BASELINE.json): aggregated peer-update GB/s (% HBM peak) at 1/2/4/8
+MI355X.  Default workload = cfg3's per-GPU coordinate tile: 256 peers x 125M
+fp32 coordinates PER GPU (weak scaling; at 8 GPUs the job is exactly cfg3,
+1B coordinates x 256 peers).  cfg3 itself (1.02 TB of peer data) does not fit
+one GPU's 288 GB, so a GPU owns one 125M-coordinate tile (128 GB resident).
+
+A step = one FedAvg pass (sum of K peers in list order, /K, w += 0.1*mean)
+over the resident tile; at N > 1 each rank reduces its round-robin coordinate
+chunks and an RCCL all-gather (over xGMI) reassembles the global model,
+pipelined per chunk on a second stream.  Inputs are generated on device by
+the counter PRNG before timing; nothing is skipped inside the timed region.
+
+value = peer-update bytes consumed by all ranks / step time (GB/s).
+roofline.achieved = algorithmic bytes per launch 4n(K+2) / mean kernel time
+(HIP events on the launch stream), peak 8.0 TB/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from p2pdl_amd import ops  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+W_PEER, UPD_SCALE, W_SCALE = 0xFFFFF, 1e-2, 5e-2
+
+WORKLOADS = {
+    # name: (rule, peers, coords per GPU, seed)
+    "cfg3": ("fedavg", 256, 125_000_000, 0x5EED0002),
+    "cfg2": ("fedavg", 64, 11_689_512, 0x5EED0001),
+    "cfg4-median": ("median", 128, 100_000_000, 0x5EED0003),
+    "cfg4-trimmed": ("trimmed", 128, 100_000_000, 0x5EED0003),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
+    ap.add_argument("--coords", type=int, default=0, help="override coordinates per GPU")
+    ap.add_argument("--peers", type=int, default=0, help="override K")
+    ap.add_argument("--chunks", type=int, default=8, help="all-gather pipeline chunks per rank (N>1)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    rule, K, n, seed = WORKLOADS[args.workload]
+    K = args.peers or K
+    n = args.coords or n
+    S = args.chunks if world > 1 else 1
+    C = -(-n // S)
+    n = C * S  # whole chunks per rank
+    free, total = torch.cuda.mem_get_info(dev)
+    need = (K + 2 + world) * n * 4
+    if need > free * 0.97:
+        raise SystemExit(f"workload needs {need/1e9:.1f} GB, {free/1e9:.1f} GB free")
+
+    # ---- synthetic inputs, resident in HBM (outside the timed region) ----
+    log(f"[rank {rank}] generating {K} x {n:,} fp32 peer slab ({K*n*4/1e9:.1f} GB)")
+    slab = torch.empty((K, n), dtype=torch.float32, device=dev)
+    for p in range(K):
+        ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE, C, world, rank)
+    w = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.fill_synthetic_(w, seed, W_PEER, W_SCALE, C, world, rank)
+    w_full = torch.empty(n * world, dtype=torch.float32, device=dev) if world > 1 else None
+    tables = [ops.pointer_table([slab[p, s * C:(s + 1) * C] for p in range(K)], dev) for s in range(S)]
+    torch.cuda.synchronize()
+
+    comp = torch.cuda.current_stream(dev)
+    comm = torch.cuda.Stream(dev)
+    kern_events = []  # (start, end) per kernel launch, on the launch stream
+
+    def step(record=False):
+        for s in range(S):
+            ws = w[s * C:(s + 1) * C]
+            if record:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(comp)
+            ops.aggregate(None, rule, w=ws, lr=0.1, table=tables[s])
+            if record:
+                e1.record(comp)
+                kern_events.append((e0, e1))
+            if world > 1:
+                done = torch.cuda.Event()
+                done.record(comp)
+                comm.wait_event(done)
+                with torch.cuda.stream(comm):
+                    dist.all_gather_into_tensor(w_full[s * C * world:(s + 1) * C * world], ws)
+        if world > 1:
+            comp.wait_stream(comm)
+
+    # ---- correctness spot check of the first warmup step vs the oracle ----
+    check = None
+    if not args.no_check and rank == 0:
+        m = min(4096, C)
+        check = (w[:m].cpu().numpy().copy(), m)
+    for i in range(max(args.warmup, 1 if check else 0)):
+        step()
+        if i == 0 and check is not None:
+            torch.cuda.synchronize()
+            import numpy as np
+
+            import oracle  # checker only
+            w0, m = check
+            peers = [oracle.synth(m, seed, p, UPD_SCALE, C, world, rank) for p in range(K)]
+            rid = ops.rule_id(rule)
+            if rid == 0:
+                want, _ = oracle.fedavg(peers, w0)
+            else:
+                want, _ = oracle.robust(peers, rid, ops.trim_count(K) if rid == 2 else 0, w=w0)
+            got = w[:m].cpu().numpy()
+            ok = np.array_equal(got.view(np.uint32), want.view(np.uint32))
+            log(f"[rank 0] spot check vs oracle ({m} coords): {'bit-exact' if ok else 'MISMATCH'}")
+            if not ok:
+                raise SystemExit("bench: kernel output differs from the oracle")
+
+    # ---- timed region ----
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = sum(a.elapsed_time(b) for a, b in kern_events) / len(kern_events)
+
+    step_s = elapsed / args.steps
+    peer_bytes = K * n * 4 * world
+    value = peer_bytes / step_s / 1e9
+    launch_n = C
+    alg_bytes = 4 * launch_n * (K + 2)
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+
+    traffic = None
+    tfile = os.path.join(REPO, "profiles", f"traffic_{args.workload}.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tj = json.load(f)
+        if tj.get("coords_per_launch") == launch_n and tj.get("peers") == K:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle.cpu_baseline as cb  # baseline leg only
+
+        torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+        n_s = 1_000_000
+        if rule == "fedavg":
+            gbs, thr, reps, el = cb.time_fedavg(K, n_s, args.cpu_seconds)
+        else:
+            gbs, thr, reps, el = cb.time_median(K, n_s, args.cpu_seconds)
+        cpu = {"value": round(gbs, 3), "unit": "GB/s", "cores": thr, "kind": "port",
+               "sample": f"{K} peers x {n_s:,} fp32 coords, reference op sequence "
+                         f"(aggregation.py:15-38) on torch CPU, {reps} reps in {el:.1f}s"}
+
+    if rank == 0:
+        line = {
+            "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (device counter PRNG, SURVEY.md §8(d)); random-init model weights",
+            "config": {"workload": f"{args.workload}: {rule} over {K} peers x {n:,} fp32 coords per GPU"
+                                   + (" (cfg3 per-GPU tile; N=8 -> 1B coords)" if args.workload == "cfg3" else ""),
+                       "rule": rule, "peers": K, "coords_per_gpu": n, "coords_total": n * world,
+                       "parallelism": f"coord-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                       "pct_hbm_peak_step": round(4 * n * (K + 2) * world / step_s / 1e9 / world / HBM_PEAK_GBS, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,129 @@
+/*
+ * p2pdl.h -- C ABI of the MI355X (gfx950) aggregation / digest hot path.
+ *
+ * Drop-in boundary for P2PDL's data-parallel hot path.
+ * Plain pointers and sizes only: no torch / C++ types cross this ABI.  The
+ * Python host layer (p2pdl_amd/_native.py) binds these with ctypes; the
+ * binding a maintainer would add to the reference is in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every pointer named peers / w / out / msgs / lens / digests is a DEVICE
+ *     pointer.  `peers` is a device array of K device pointers, one per peer
+ *     update, in the order of the reference's received_models list
+ *     (reference node/node.py:141 appends in arrival order; the reference
+ *     sums in that order, aggregator/aggregation.py:25).
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  All calls are
+ *     asynchronous, stream-ordered, allocate nothing and keep no state
+ *     (re-entrant; safe inside hipGraph capture).
+ *   - Return value: 0 = OK; < 0 = library error (P2P_ERR_*); > 0 = the
+ *     hipError_t of a failed launch.  p2p_strerror() describes any code.
+ *     No exception ever crosses the ABI.
+ *   - Numerics are bit-exact to the reference CPU op sequence:
+ *     +0 accumulator init, fixed peer order, IEEE true division by K, and
+ *     w + lr*agg with the multiply and the add separately rounded (no FMA).
+ */
+#ifndef P2PDL_H
+#define P2PDL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define P2P_ABI_VERSION 1
+
+typedef void *p2p_stream_t; /* hipStream_t */
+
+enum {
+  P2P_OK = 0,
+  P2P_ERR_INVALID = -1,     /* bad argument (null pointer, k < 1, n < 0, bad trim) */
+  P2P_ERR_UNSUPPORTED = -2, /* valid but unsupported here (robust rules need k <= 256) */
+  P2P_ERR_ALIGN = -3        /* a float pointer that is not 4-byte aligned */
+};
+
+enum { P2P_RULE_FEDAVG = 0, P2P_RULE_MEDIAN = 1, P2P_RULE_TRIMMED = 2 };
+
+/* One tensor of a state_dict (reference: one key of self.model.state_dict(),
+ * aggregator/aggregation.py:15,27,37).  Device-resident table entry. */
+typedef struct p2p_segment_t {
+  const float *const *peers; /* device array of K device pointers: this key of each update */
+  float *w;                  /* model tensor for this key, updated in place (nullable) */
+  float *out;                /* receives the aggregate before apply (nullable) */
+  int64_t n;                 /* elements in this tensor */
+  int64_t tile_begin;        /* sum of ceil(n_j / p2p_tile_elems(rule)) over earlier segments */
+} p2p_segment_t;
+
+/* ABI version (P2P_ABI_VERSION) and error text (static storage). */
+int32_t p2p_abi_version(void);
+const char *p2p_strerror(int32_t code);
+
+/* Elements per tile of the segment kernel for `rule` (host planning helper). */
+int64_t p2p_tile_elems(int32_t rule);
+
+/* ---- K1: FedAvg --------------------------------------------------------
+ * Replaces reference aggregator/aggregation.py:15-38 for one flat buffer:
+ *   acc = +0 (:15); acc += peers[j] for j in list order (:25-28);
+ *   acc /= K (:31-32); w += fp32(lr) * acc (:36-38, lr = 0.1 there). */
+int32_t p2p_fedavg_apply_f32(const float *const *peers, int32_t k, int64_t n, float *w, float lr,
+                             p2p_stream_t stream);
+/* Same reduction, writes acc/K to out (the :15-32 part, no apply). */
+int32_t p2p_mean_f32(const float *const *peers, int32_t k, int64_t n, float *out,
+                     p2p_stream_t stream);
+/* FedAvg over a device-resident peer count: K = *k_dev (1 <= K <= k_max),
+ * peers[0..K-1] used.  Feeds the fused digest -> accept -> FedAvg path. */
+int32_t p2p_fedavg_apply_devk_f32(const float *const *peers, const int32_t *k_dev, int32_t k_max,
+                                  int64_t n, float *w, float lr, float *out, p2p_stream_t stream);
+
+/* ---- K2: robust rules (build-defined: reference README.md:10 TODO) -----
+ * median: rank (K-1)/2 under the IEEE total order on float bits.
+ * trimmed: ascending fp32 sum of sorted ranks b..K-b-1 from +0, / (K-2b).
+ * k <= 256. */
+int32_t p2p_median_f32(const float *const *peers, int32_t k, int64_t n, float *out,
+                       p2p_stream_t stream);
+int32_t p2p_trimmed_mean_f32(const float *const *peers, int32_t k, int64_t n, int32_t trim_b,
+                             float *out, p2p_stream_t stream);
+
+/* Generic fused form of K1/K2: rule in P2P_RULE_*; writes the aggregate to
+ * out (nullable) and applies w += lr*agg when w is non-null (at least one of
+ * w, out must be non-null).  trim_b is read only for P2P_RULE_TRIMMED. */
+int32_t p2p_aggregate_f32(const float *const *peers, int32_t k, int64_t n, int32_t rule,
+                          int32_t trim_b, float lr, float *w, float *out, p2p_stream_t stream);
+
+/* Whole state_dict in ONE launch: segs is a DEVICE array of nseg entries
+ * (tile_begin prefix-summed with p2p_tile_elems(rule)); total_tiles is the
+ * sum over all segments.  Replaces the per-key loops of
+ * aggregator/aggregation.py:15,25-28,31-32,37-38. */
+int32_t p2p_aggregate_segments_f32(const p2p_segment_t *segs, int32_t nseg, int64_t total_tiles,
+                                   int32_t k, int32_t rule, int32_t trim_b, float lr,
+                                   p2p_stream_t stream);
+
+/* w += lr * agg, multiply and add separately rounded (aggregation.py:36-38). */
+int32_t p2p_apply_f32(float *w, const float *agg, float lr, int64_t n, p2p_stream_t stream);
+
+/* ---- K3: SHA-256 over serialized updates --------------------------------
+ * digests[32*i .. 32*i+31] = SHA-256(msgs[i][0 .. lens[i]-1]) (FIPS 180-4),
+ * the digest inside ECDSA(SHA256()) of reference utils/crypto.py:54-57 (sign)
+ * and :92-96 (verify).  msgs, lens, digests are device arrays. */
+int32_t p2p_sha256_batch(const uint8_t *const *msgs, const uint64_t *lens, int32_t k,
+                         uint8_t *digests, p2p_stream_t stream);
+
+/* Accept step of the fused path: keeps peer i iff digests[i] == expected[i]
+ * (32 bytes each); writes the kept payload pointers, in the original list
+ * order, to accepted[0..count-1] and count to *count (both device). */
+int32_t p2p_digest_accept(const uint8_t *digests, const uint8_t *expected,
+                          const float *const *payloads, int32_t k, const float **accepted,
+                          int32_t *count, p2p_stream_t stream);
+
+/* ---- synthetic inputs ---------------------------------
+ * out[i] = ((splitmix64(seed ^ (peer << 40) ^ g(i)) >> 40) * 2^-23 - 1) * scale
+ * with g(i) the global coordinate of local element i under round-robin chunk
+ * ownership (chunk elements per chunk; g(i) = i when nranks <= 1). */
+int32_t p2p_fill_synthetic_f32(float *out, int64_t n, uint64_t seed, int32_t peer, float scale,
+                               int64_t chunk, int32_t nranks, int32_t rank, p2p_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* P2PDL_H */

@@ -1,0 +1,217 @@
+// K1 -- streaming K-peer FedAvg reduction + apply for gfx950.
+//
+// Replaces reference aggregator/aggregation.py:15-38:
+//   acc = zeros_like(p)                         (:15)  -> acc = +0 in registers
+//   for upd in received_models: acc += upd[key]  (:25-28) -> fixed peer order
+//   acc /= num_updates                           (:31-32) -> IEEE true division
+//   state_dict()[key] += 0.1 * acc               (:36-38) -> mul rounded, add rounded
+//
+// The reference issues K*L separate add_ kernels, each reading acc + update and
+// writing acc (3x the algorithmic traffic).  Here one pass reads every peer
+// element once, keeps the running sum in VGPRs and touches w once:
+// algorithmic bytes = 4*n*(K+2) per launch (K peer reads + w read + w write).
+//
+// Layout: a lane owns kVec=8 consecutive floats (two 16-B dwordx4 loads per
+// peer); a 256-lane block owns a 2048-float tile.  The peer loop is unrolled
+// kUnroll deep so each lane keeps 2*kUnroll 16-B loads in flight.  Peer
+// streams are read once -> nontemporal loads.  No inter-block reuse exists,
+// so no XCD remap is needed (guide T1: 0% on elementwise).
+#include "p2p_common.h"
+
+namespace p2p {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kVec = 8;
+constexpr int kTile = kBlock * kVec;  // 2048 floats per tile
+constexpr int kUnroll = 8;
+
+__device__ __forceinline__ f4 ld_nt(const float* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+}
+__device__ __forceinline__ f4 ld(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ void st(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
+__device__ __forceinline__ f4 div4(f4 a, float k) {
+  f4 r;
+  r.x = a.x / k; r.y = a.y / k; r.z = a.z / k; r.w = a.w / k;
+  return r;
+}
+__device__ __forceinline__ f4 apply4(f4 w, float lr, f4 m) {
+  f4 r;
+  r.x = apply_lr(w.x, lr, m.x); r.y = apply_lr(w.y, lr, m.y);
+  r.z = apply_lr(w.z, lr, m.z); r.w = apply_lr(w.w, lr, m.w);
+  return r;
+}
+
+// Wave-uniform: are all peer pointers (and w/out) 16-B aligned?
+__device__ __forceinline__ bool all_aligned16(const float* const* peers, int K, const float* w,
+                                              const float* out) {
+  uintptr_t m = reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(out);
+  for (int k = 0; k < K; ++k) m |= reinterpret_cast<uintptr_t>(peers[k]);
+  return (m & 15) == 0;
+}
+
+// One tile, one lane's 8 elements starting at `base` (< n).
+__device__ __forceinline__ void fedavg_lane(const float* const* __restrict__ peers, int K,
+                                            int64_t n, int64_t base, float* w, float* out,
+                                            float lr, bool aligned) {
+  const float fk = static_cast<float>(K);
+  if (aligned && base + kVec <= n) {
+    f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
+    int k = 0;
+    for (; k + kUnroll <= K; k += kUnroll) {
+      f4 x0[kUnroll], x1[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const float* p = peers[k + u] + base;
+        x0[u] = ld_nt(p);
+        x1[u] = ld_nt(p + 4);
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {  // strictly in list order (:25-28)
+        a0 += x0[u];
+        a1 += x1[u];
+      }
+    }
+    for (; k < K; ++k) {
+      const float* p = peers[k] + base;
+      a0 += ld_nt(p);
+      a1 += ld_nt(p + 4);
+    }
+    const f4 m0 = div4(a0, fk), m1 = div4(a1, fk);  // (:31-32)
+    if (out) {
+      st(out + base, m0);
+      st(out + base + 4, m1);
+    }
+    if (w) {  // (:36-38)
+      st(w + base, apply4(ld(w + base), lr, m0));
+      st(w + base + 4, apply4(ld(w + base + 4), lr, m1));
+    }
+    return;
+  }
+  // tail or unaligned: scalar path, same op order
+  const int cnt = static_cast<int>(n - base < kVec ? n - base : kVec);
+  for (int e = 0; e < cnt; ++e) {
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc += peers[k][base + e];
+    const float m = acc / fk;
+    if (out) out[base + e] = m;
+    if (w) w[base + e] = apply_lr(w[base + e], lr, m);
+  }
+}
+
+// Flat buffer, grid-stride over tiles.  K either from the kernarg or, when
+// k_dev != nullptr, from device memory (fused accept -> FedAvg path).
+__global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const* __restrict__ peers,
+                                                             int K, const int32_t* k_dev,
+                                                             int64_t n, float* w, float* out,
+                                                             float lr) {
+  if (k_dev) K = *k_dev;
+  if (K <= 0) return;
+  const bool aligned = all_aligned16(peers, K, w, out);
+  const int64_t ntiles = ceil_div(n, kTile);
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t base = t * kTile + static_cast<int64_t>(threadIdx.x) * kVec;
+    if (base < n) fedavg_lane(peers, K, n, base, w, out, lr, aligned);
+  }
+}
+
+// Whole state_dict: one tile per block, segment found by binary search.
+__global__ __launch_bounds__(kBlock) void fedavg_segments_kernel(const Seg* __restrict__ segs,
+                                                                 int nseg, int K, float lr) {
+  const int64_t t = blockIdx.x;
+  const Seg& s = segs[find_segment(segs, nseg, t)];
+  const int64_t base = (t - s.tile_begin) * kTile + static_cast<int64_t>(threadIdx.x) * kVec;
+  if (base >= s.n) return;
+  const bool aligned = all_aligned16(s.peers, K, s.w, s.out);
+  fedavg_lane(s.peers, K, s.n, base, s.w, s.out, lr, aligned);
+}
+
+__global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* agg, float lr,
+                                                       int64_t n) {
+  const bool aligned = ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(agg)) & 15) == 0;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock * 4;
+  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4; i < n; i += stride) {
+    if (aligned && i + 4 <= n) {
+      st(w + i, apply4(ld(w + i), lr, ld(agg + i)));
+    } else {
+      for (int64_t j = i; j < n && j < i + 4; ++j) w[j] = apply_lr(w[j], lr, agg[j]);
+    }
+  }
+}
+
+static int grid_for_tiles(int64_t ntiles) {
+  // 256 CUs x 8 blocks of 256 lanes = full residency; grid-stride beyond.
+  const int64_t cap = 256 * 8;
+  return static_cast<int>(ntiles < cap ? (ntiles > 0 ? ntiles : 1) : cap);
+}
+
+}  // namespace p2p
+
+using namespace p2p;
+
+static int32_t launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? P2P_OK : static_cast<int32_t>(e);
+}
+
+extern "C" P2P_INTERNAL int64_t p2p_fedavg_tile_elems(void) { return kTile; }
+
+P2P_INTERNAL int32_t p2p_fedavg_flat_launch(const float* const* peers, int32_t k, int64_t n, float* w,
+                                            float* out, float lr, p2p_stream_t stream) {
+  hipLaunchKernelGGL(fedavg_flat_kernel, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), peers, k, nullptr, n, w, out, lr);
+  return launch_status();
+}
+
+extern "C" int32_t p2p_fedavg_apply_f32(const float* const* peers, int32_t k, int64_t n, float* w,
+                                        float lr, p2p_stream_t stream) {
+  if (!peers || !w || k < 1 || n < 0) return P2P_ERR_INVALID;
+  if (reinterpret_cast<uintptr_t>(w) & 3) return P2P_ERR_ALIGN;
+  if (n == 0) return P2P_OK;
+  hipLaunchKernelGGL(fedavg_flat_kernel, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), peers, k, nullptr, n, w, nullptr, lr);
+  return launch_status();
+}
+
+extern "C" int32_t p2p_mean_f32(const float* const* peers, int32_t k, int64_t n, float* out,
+                                p2p_stream_t stream) {
+  if (!peers || !out || k < 1 || n < 0) return P2P_ERR_INVALID;
+  if (reinterpret_cast<uintptr_t>(out) & 3) return P2P_ERR_ALIGN;
+  if (n == 0) return P2P_OK;
+  hipLaunchKernelGGL(fedavg_flat_kernel, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), peers, k, nullptr, n, nullptr, out, 0.f);
+  return launch_status();
+}
+
+extern "C" int32_t p2p_fedavg_apply_devk_f32(const float* const* peers, const int32_t* k_dev,
+                                             int32_t k_max, int64_t n, float* w, float lr,
+                                             float* out, p2p_stream_t stream) {
+  if (!peers || !k_dev || (!w && !out) || k_max < 1 || n < 0) return P2P_ERR_INVALID;
+  if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(out)) & 3) return P2P_ERR_ALIGN;
+  if (n == 0) return P2P_OK;
+  hipLaunchKernelGGL(fedavg_flat_kernel, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), peers, k_max, k_dev, n, w, out, lr);
+  return launch_status();
+}
+
+extern "C" P2P_INTERNAL int32_t p2p_fedavg_segments_f32(const p2p_segment_t* segs, int32_t nseg,
+                                           int64_t total_tiles, int32_t k, float lr,
+                                           p2p_stream_t stream) {
+  if (!segs || nseg < 1 || k < 1 || total_tiles < 0) return P2P_ERR_INVALID;
+  if (total_tiles == 0) return P2P_OK;
+  hipLaunchKernelGGL(fedavg_segments_kernel, dim3(static_cast<unsigned>(total_tiles)), dim3(kBlock),
+                     0, static_cast<hipStream_t>(stream), segs, nseg, k, lr);
+  return launch_status();
+}
+
+extern "C" int32_t p2p_apply_f32(float* w, const float* agg, float lr, int64_t n,
+                                 p2p_stream_t stream) {
+  if (!w || !agg || n < 0) return P2P_ERR_INVALID;
+  if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(agg)) & 3) return P2P_ERR_ALIGN;
+  if (n == 0) return P2P_OK;
+  hipLaunchKernelGGL(apply_kernel, dim3(grid_for_tiles(ceil_div(n, kBlock * 4))), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), w, agg, lr, n);
+  return launch_status();
+}

@@ -1,0 +1,274 @@
+"""Tensor-level entry points to the gfx950 kernels (via the C ABI).
+
+All functions take torch tensors that already live on a ROCm device, launch
+on ``torch.cuda.current_stream()`` and return without synchronising (except
+where a host result is requested, e.g. ``sha256_batch`` returning bytes).
+Peer tensors are never stacked or copied: the kernels read them through a
+device-resident table of K base pointers (SURVEY.md §8(b) "Ownership").
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+from ._native import P2P_RULE_FEDAVG, P2P_RULE_MEDIAN, P2P_RULE_TRIMMED
+
+RULES = {"fedavg": P2P_RULE_FEDAVG, "mean": P2P_RULE_FEDAVG, "median": P2P_RULE_MEDIAN,
+         "trimmed": P2P_RULE_TRIMMED, "trimmed_mean": P2P_RULE_TRIMMED}
+MAX_ROBUST_PEERS = 256
+DEFAULT_TRIM_FRAC = 0.2
+
+
+def rule_id(rule) -> int:
+    if isinstance(rule, int):
+        if rule not in (0, 1, 2):
+            raise ValueError(f"unknown aggregation rule id {rule}")
+        return rule
+    try:
+        return RULES[str(rule).lower()]
+    except KeyError:
+        raise ValueError(f"unknown aggregation rule {rule!r}; expected one of {sorted(RULES)}") from None
+
+
+def trim_count(k: int, trim_frac: float = DEFAULT_TRIM_FRAC) -> int:
+    """b = floor(trim_frac * K); the epsilon keeps exact
+    products such as 0.2*5 from landing one ulp under an integer."""
+    b = int(math.floor(trim_frac * k + 1e-9))
+    if b < 0 or k - 2 * b < 1:
+        raise ValueError(f"trim_frac={trim_frac} leaves no ranks for K={k}")
+    return b
+
+
+def _check_f32(t: torch.Tensor, name: str, device) -> None:
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+    if t.device != device:
+        raise RuntimeError(f"{name}: expected all tensors on {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+
+
+def pointer_table(tensors: Sequence[torch.Tensor], device) -> torch.Tensor:
+    """Device int64 tensor of data pointers (one small H2D copy)."""
+    host = torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64)
+    return host.to(device, non_blocking=False)
+
+
+def _peer_inputs(peers: Sequence[torch.Tensor], n: int, device):
+    if len(peers) == 0:
+        raise ValueError("need at least one peer update")
+    for i, p in enumerate(peers):
+        _check_f32(p, f"peers[{i}]", device)
+        if p.numel() != n:
+            raise ValueError(f"peers[{i}] has {p.numel()} elements, expected {n}")
+    return pointer_table(peers, device)
+
+
+# ------------------------------------------------------------------ K1 / K2
+def aggregate(peers: Sequence[torch.Tensor], rule="fedavg", *, w: torch.Tensor | None = None,
+              out: torch.Tensor | None = None, lr: float = 0.1, trim_b: int | None = None,
+              trim_frac: float = DEFAULT_TRIM_FRAC, table: torch.Tensor | None = None) -> None:
+    """One flat buffer: out = rule(peers); w += lr * out (when w is given).
+
+    ``table`` may pass a prebuilt device pointer table (benchmarks reuse it)."""
+    ref = w if w is not None else out
+    if ref is None:
+        raise ValueError("need w and/or out")
+    N.require_device(ref)
+    n = ref.numel()
+    for name, t in (("w", w), ("out", out)):
+        if t is not None:
+            _check_f32(t, name, ref.device)
+            if t.numel() != n:
+                raise ValueError(f"{name} has {t.numel()} elements, expected {n}")
+    r = rule_id(rule)
+    k = len(peers) if table is None else table.numel()
+    if table is None:
+        table = _peer_inputs(peers, n, ref.device)
+    if r != P2P_RULE_FEDAVG and k > MAX_ROBUST_PEERS:
+        raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {k}")
+    b = 0
+    if r == P2P_RULE_TRIMMED:
+        b = trim_count(k, trim_frac) if trim_b is None else int(trim_b)
+    with torch.cuda.device(ref.device):
+        N.check(N.lib().p2p_aggregate_f32(table.data_ptr(), k, n, r, b, lr,
+                                          w.data_ptr() if w is not None else None,
+                                          out.data_ptr() if out is not None else None,
+                                          N.stream_handle()), "p2p_aggregate_f32")
+
+
+def fedavg_apply_(w: torch.Tensor, peers: Sequence[torch.Tensor], lr: float = 0.1) -> torch.Tensor:
+    """w += lr * mean(peers) in place (reference aggregation.py:15-38)."""
+    aggregate(peers, "fedavg", w=w, lr=lr)
+    return w
+
+
+def mean(peers: Sequence[torch.Tensor]) -> torch.Tensor:
+    out = torch.empty_like(peers[0])
+    aggregate(peers, "fedavg", out=out)
+    return out
+
+
+def median(peers: Sequence[torch.Tensor]) -> torch.Tensor:
+    out = torch.empty_like(peers[0])
+    aggregate(peers, "median", out=out)
+    return out
+
+
+def trimmed_mean(peers: Sequence[torch.Tensor], trim_frac: float = DEFAULT_TRIM_FRAC,
+                 trim_b: int | None = None) -> torch.Tensor:
+    out = torch.empty_like(peers[0])
+    aggregate(peers, "trimmed", out=out, trim_frac=trim_frac, trim_b=trim_b)
+    return out
+
+
+def apply_(w: torch.Tensor, agg: torch.Tensor, lr: float = 0.1) -> torch.Tensor:
+    N.require_device(w)
+    _check_f32(w, "w", w.device)
+    _check_f32(agg, "agg", w.device)
+    if agg.numel() != w.numel():
+        raise ValueError("w and agg differ in size")
+    with torch.cuda.device(w.device):
+        N.check(N.lib().p2p_apply_f32(w.data_ptr(), agg.data_ptr(), lr, w.numel(),
+                                      N.stream_handle()), "p2p_apply_f32")
+    return w
+
+
+# ----------------------------------------------------- whole state_dict
+_SEG_DTYPE = np.dtype([("peers", "<u8"), ("w", "<u8"), ("out", "<u8"), ("n", "<i8"),
+                       ("tile_begin", "<i8")])  # == p2p_segment_t (40 B)
+
+
+def aggregate_segments_(ws: Sequence[torch.Tensor], peer_lists: Sequence[Sequence[torch.Tensor]],
+                        rule="fedavg", *, lr: float = 0.1, trim_b: int | None = None,
+                        trim_frac: float = DEFAULT_TRIM_FRAC,
+                        outs: Sequence[torch.Tensor] | None = None) -> None:
+    """All L tensors of a state_dict in ONE launch.
+
+    ws[l] is updated in place with lr * rule(peer_lists[j][l] for j in peers);
+    peer_lists[j] is the j-th update's tensors in the same key order."""
+    L = len(ws)
+    if L == 0:
+        return
+    K = len(peer_lists)
+    if K == 0:
+        raise ValueError("need at least one peer update")
+    dev = ws[0].device
+    N.require_device(ws[0])
+    r = rule_id(rule)
+    if r != P2P_RULE_FEDAVG and K > MAX_ROBUST_PEERS:
+        raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {K}")
+    b = trim_count(K, trim_frac) if (r == P2P_RULE_TRIMMED and trim_b is None) else int(trim_b or 0)
+    tile = int(N.lib().p2p_tile_elems(r))
+    segs = np.zeros(L, dtype=_SEG_DTYPE)
+    ptrs = np.zeros((L, K), dtype=np.uint64)
+    tiles = 0
+    for l, w in enumerate(ws):
+        _check_f32(w, f"w[{l}]", dev)
+        n = w.numel()
+        for j in range(K):
+            p = peer_lists[j][l]
+            _check_f32(p, f"update[{j}][{l}]", dev)
+            if p.numel() != n:
+                raise ValueError(f"update[{j}][{l}] has {p.numel()} elements, expected {n}")
+            ptrs[l, j] = p.data_ptr()
+        segs[l]["w"] = w.data_ptr()
+        segs[l]["out"] = outs[l].data_ptr() if outs is not None else 0
+        segs[l]["n"] = n
+        segs[l]["tile_begin"] = tiles
+        tiles += -(-n // tile)
+    seg_bytes = segs.nbytes
+    buf = torch.empty(seg_bytes + ptrs.nbytes, dtype=torch.uint8, device=dev)
+    base = buf.data_ptr()
+    segs["peers"] = base + seg_bytes + np.arange(L, dtype=np.uint64) * np.uint64(8 * K)
+    host = np.concatenate([segs.view(np.uint8), ptrs.view(np.uint8).reshape(-1)])
+    buf.copy_(torch.from_numpy(host))
+    if tiles == 0:
+        return
+    with torch.cuda.device(dev):
+        N.check(N.lib().p2p_aggregate_segments_f32(base, L, tiles, K, r, b, lr, N.stream_handle()),
+                "p2p_aggregate_segments_f32")
+    # keep the table alive until the kernel has consumed it (stream-ordered reuse)
+    buf.record_stream(torch.cuda.current_stream(dev))
+
+
+# ------------------------------------------------------------------ K3
+def sha256_batch_device(msgs: torch.Tensor, offsets: Sequence[int], lengths: Sequence[int]) -> torch.Tensor:
+    """Digest K messages that live in one device uint8 buffer.
+
+    Returns a (K, 32) uint8 device tensor; does not synchronise."""
+    N.require_device(msgs)
+    dev = msgs.device
+    K = len(offsets)
+    digests = torch.empty((max(K, 1), 32), dtype=torch.uint8, device=dev)
+    if K == 0:
+        return digests[:0]
+    base = msgs.data_ptr()
+    ptrs = torch.tensor([base + int(o) for o in offsets], dtype=torch.int64).to(dev)
+    lens = torch.tensor([int(x) for x in lengths], dtype=torch.int64).to(dev)
+    with torch.cuda.device(dev):
+        N.check(N.lib().p2p_sha256_batch(ptrs.data_ptr(), lens.data_ptr(), K, digests.data_ptr(),
+                                         N.stream_handle()), "p2p_sha256_batch")
+    return digests
+
+
+def pack_messages(messages: Iterable[bytes], align: int = 16):
+    """Concatenate byte strings at `align`-byte offsets into one host buffer."""
+    messages = list(messages)
+    offsets, o = [], 0
+    for m in messages:
+        offsets.append(o)
+        o += -(-max(len(m), 1) // align) * align
+    host = np.zeros(max(o, align), dtype=np.uint8)
+    for off, m in zip(offsets, messages):
+        if m:
+            host[off:off + len(m)] = np.frombuffer(m, dtype=np.uint8)
+    return host, offsets, [len(m) for m in messages]
+
+
+def sha256_batch(messages: Sequence[bytes], device=None) -> list[bytes]:
+    """SHA-256 of every message on the GPU (one H2D copy, one launch)."""
+    if device is None:
+        if not torch.cuda.is_available():
+            raise N.NativeUnavailable("p2pdl_amd: no ROCm GPU visible; the HIP hot path cannot run")
+        device = torch.device("cuda", torch.cuda.current_device())
+    host, offsets, lens = pack_messages(messages)
+    dev_buf = torch.from_numpy(host).to(device)
+    d = sha256_batch_device(dev_buf, offsets, lens).cpu().numpy()
+    return [bytes(d[i]) for i in range(len(lens))]
+
+
+def digest_accept(digests: torch.Tensor, expected: torch.Tensor, payload_table: torch.Tensor,
+                  accepted: torch.Tensor, count: torch.Tensor) -> None:
+    """accepted[0:count] = payloads whose digest matches, in list order (device)."""
+    k = payload_table.numel()
+    with torch.cuda.device(digests.device):
+        N.check(N.lib().p2p_digest_accept(digests.data_ptr(), expected.data_ptr(),
+                                          payload_table.data_ptr(), k, accepted.data_ptr(),
+                                          count.data_ptr(), N.stream_handle()), "p2p_digest_accept")
+
+
+def fedavg_apply_devk_(w: torch.Tensor, table: torch.Tensor, k_dev: torch.Tensor, k_max: int,
+                       lr: float = 0.1, out: torch.Tensor | None = None) -> None:
+    """FedAvg over table[0:*k_dev] with the peer count read on the device."""
+    with torch.cuda.device(w.device):
+        N.check(N.lib().p2p_fedavg_apply_devk_f32(table.data_ptr(), k_dev.data_ptr(), k_max, w.numel(),
+                                                  w.data_ptr(), lr,
+                                                  out.data_ptr() if out is not None else None,
+                                                  N.stream_handle()), "p2p_fedavg_apply_devk_f32")
+
+
+# ------------------------------------------------------------- synthetic
+def fill_synthetic_(out: torch.Tensor, seed: int, peer: int, scale: float, chunk: int = 0,
+                    nranks: int = 1, rank: int = 0) -> torch.Tensor:
+    N.require_device(out)
+    _check_f32(out, "out", out.device)
+    with torch.cuda.device(out.device):
+        N.check(N.lib().p2p_fill_synthetic_f32(out.data_ptr(), out.numel(), seed, peer, scale,
+                                               chunk, nranks, rank, N.stream_handle()),
+                "p2p_fill_synthetic_f32")
+    return out

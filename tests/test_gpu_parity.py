@@ -1,0 +1,304 @@
+"""GPU parity: the HIP kernels (through the C ABI) vs the oracle / goldens.
+
+Bar: bit-exact float32 for FedAvg, median, trimmed mean and the apply;
+byte-exact for SHA-256.  NaN payloads produced by arithmetic compare as a
+class (see helpers.assert_bits_equal).
+"""
+import hashlib
+import os
+import pickle
+import types
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import assert_bits_equal, case_inputs, load_golden
+from p2pdl_amd import ops
+from p2pdl_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+# ------------------------------------------------------------------ basics
+def test_abi_version_and_errors(cuda):
+    L = N.load_library()
+    assert L.p2p_abi_version() == N.ABI_VERSION
+    assert b"invalid" in L.p2p_strerror(-1)
+    assert L.p2p_fedavg_apply_f32(None, 1, 10, None, 0.1, None) == -1
+    assert L.p2p_median_f32(None, 300, 10, None, None) == -1
+
+
+@pytest.mark.parametrize("n,seed,peer,scale,chunk,nranks,rank", [
+    (100_003, 0x5EED0001, 0, 1e-2, 0, 1, 0),
+    (4097, 7, 255, 5e-2, 0, 1, 0),
+    (10_000, 9, 3, 1.0, 512, 4, 3),
+])
+def test_synthetic_matches_oracle(cuda, n, seed, peer, scale, chunk, nranks, rank):
+    t = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.fill_synthetic_(t, seed, peer, scale, chunk, nranks, rank)
+    assert_bits_equal(host(t), oracle.synth(n, seed, peer, scale, chunk, nranks, rank), what="synth")
+
+
+# ------------------------------------------------------------------ FedAvg
+GOLD_META, GOLD_SMALL = load_golden()
+
+
+class Holder(torch.nn.Module):
+    def __init__(self, shapes):
+        super().__init__()
+        for name, shape in shapes:
+            self.register_parameter(name.replace(".", "__"),
+                                    torch.nn.Parameter(torch.zeros(shape, dtype=torch.float32)))
+
+
+def split(vec, shapes, dev):
+    out, o = {}, 0
+    for name, shape in shapes:
+        n = int(np.prod(shape))
+        out[name.replace(".", "__")] = to_dev(vec[o:o + n].reshape(shape), dev)
+        o += n
+    return out
+
+
+def fake_node(model, updates):
+    return types.SimpleNamespace(
+        model=model, received_models=[{"model": u, "sender": ("127.0.0.1", 7001 + i)}
+                                      for i, u in enumerate(updates)],
+        trainers_list=[0] * len(updates), addr="127.0.0.1", port=7000, neighbors=[])
+
+
+def check_against_case(out, case):
+    stride = case["sample_stride"]
+    got = np.ascontiguousarray(out[::stride], dtype=np.float32)
+    want = np.array(case["sample_bits"], dtype=np.uint32).view(np.float32)
+    assert_bits_equal(got, want, what=case["name"])
+    if case["out_sha256"] is not None:
+        assert hashlib.sha256(np.ascontiguousarray(out, dtype=np.float32).tobytes()).hexdigest() \
+            == case["out_sha256"], case["name"]
+
+
+@pytest.mark.parametrize("case", GOLD_META["cases"], ids=lambda c: c["name"])
+def test_dropin_aggregate_models_matches_reference_golden(cuda, case, monkeypatch):
+    """The drop-in aggregate_models on a fake Node == the reference's output."""
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    calls = []
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: calls.append(self))
+    shapes = [(nm, tuple(s)) for nm, s in case["shapes"]]
+    w, peers = case_inputs(case, GOLD_SMALL)
+    model = Holder(shapes).to(cuda)
+    with torch.no_grad():
+        model.load_state_dict(split(w, shapes, cuda))
+    node = fake_node(model, [split(p, shapes, cuda) for p in peers])
+    assert agg.aggregate_models(node) is None
+    out = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+    check_against_case(out, case)
+    if f"{case['name']}__out" in GOLD_SMALL:
+        assert_bits_equal(out, GOLD_SMALL[f"{case['name']}__out"], what=case["name"])
+    assert node.received_models == [] and len(calls) == 1
+
+
+@pytest.mark.parametrize("case", GOLD_META["cases"], ids=lambda c: c["name"])
+def test_flat_fedavg_matches_reference_golden(cuda, case):
+    """The flat C-ABI entry (one buffer per peer) on the same golden inputs."""
+    w, peers = case_inputs(case, GOLD_SMALL)
+    wt = to_dev(w, cuda)
+    ops.fedavg_apply_(wt, [to_dev(p, cuda) for p in peers], lr=case["lr"])
+    check_against_case(host(wt), case)
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 7, 8, 9, 16, 17, 64, 255])
+@pytest.mark.parametrize("n", [1, 7, 2048, 2049, 100_003])
+def test_fedavg_vs_oracle(cuda, k, n):
+    seed = 1000 * k + n
+    peers = [oracle.synth(n, seed, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, seed, 0xFFFFF, 5e-2)
+    w_ref, out_ref = oracle.fedavg(peers, w, want_out=True)
+    wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate([to_dev(p, cuda) for p in peers], "fedavg", w=wt, out=out)
+    assert_bits_equal(host(out), out_ref, what="mean")
+    assert_bits_equal(host(wt), w_ref, what="apply")
+
+
+def test_fedavg_unaligned_views(cuda):
+    """Peers that are 4-B but not 16-B aligned take the scalar path, same bits."""
+    n, k = 5000, 5
+    raw = [oracle.synth(n + 3, 77, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, 77, 0xFFFFF, 5e-2)
+    dev_raw = [to_dev(r, cuda) for r in raw]
+    views = [d[1 + (p % 3):1 + (p % 3) + n] for p, d in enumerate(dev_raw)]
+    w_ref, _ = oracle.fedavg([r[1 + (p % 3):1 + (p % 3) + n] for p, r in enumerate(raw)], w)
+    wt = to_dev(w, cuda)
+    ops.fedavg_apply_(wt, views)
+    assert_bits_equal(host(wt), w_ref, what="unaligned")
+
+
+def test_fedavg_large_k64_resnet_shape(cuda):
+    """cfg2 shape (K=64 x 11,689,512) generated on device, checked on host."""
+    n, k, seed = 11_689_512, 64, 0x5EED0001
+    slab = torch.empty((k, n), dtype=torch.float32, device=cuda)
+    for p in range(k):
+        ops.fill_synthetic_(slab[p], seed, p, 1e-2)
+    w = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.fill_synthetic_(w, seed, 0xFFFFF, 5e-2)
+    ops.fedavg_apply_(w, list(slab))
+    got = host(w)
+    sl = slice(n - 300_007, n)  # check a tail window against the oracle (keeps CPU time small)
+    peers = [oracle.synth(n, seed, p, 1e-2)[sl] for p in range(k)]
+    w_ref, _ = oracle.fedavg(peers, oracle.synth(n, seed, 0xFFFFF, 5e-2)[sl])
+    assert_bits_equal(got[sl], w_ref, what="cfg2 tail")
+
+
+def test_fedavg_devk(cuda):
+    n, k = 9999, 6
+    peers = [to_dev(oracle.synth(n, 5, p, 1e-2), cuda) for p in range(k)]
+    table = ops.pointer_table(peers, cuda)
+    kdev = torch.tensor([4], dtype=torch.int32, device=cuda)
+    w0 = oracle.synth(n, 5, 0xFFFFF, 5e-2)
+    wt = to_dev(w0, cuda)
+    ops.fedavg_apply_devk_(wt, table, kdev, k)
+    w_ref, _ = oracle.fedavg([host(p) for p in peers[:4]], w0)
+    assert_bits_equal(host(wt), w_ref, what="devk")
+
+
+# ------------------------------------------------------------------ robust
+def special_peers(k, n, seed):
+    rng = np.random.default_rng(seed)
+    sp = np.array([0.0, -0.0, 1e-45, -1e-45, np.inf, -np.inf, np.nan, -np.nan, 1.0, -1.0,
+                   3.4e38, -3.4e38, 0.5, 0.25], dtype=np.float32)
+    peers = []
+    for p in range(k):
+        x = oracle.synth(n, seed, p, 1e-2)
+        x[: n // 4] = np.round(x[: n // 4] * 2 ** 8) / 2 ** 8 * 0  # ties (many zeros of both signs)
+        x[: n // 8] = np.where(rng.random(n // 8) < 0.5, np.float32(-0.0), np.float32(0.0))
+        m = rng.random(n) < 0.05
+        x[m] = rng.choice(sp, size=int(m.sum()))
+        q = slice(n // 4, n // 2)
+        x[q] = np.round(x[q] * 2 ** 6) / 2 ** 6  # quantised: many equal keys
+        peers.append(x.astype(np.float32))
+    return peers
+
+
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 7, 8, 15, 16, 31, 33, 64, 100, 127, 128, 129, 200, 255, 256])
+def test_robust_vs_oracle(cuda, rule, k):
+    n = 3001
+    peers = special_peers(k, n, 31 * k)
+    w = oracle.synth(n, 3, 0xFFFFF, 5e-2)
+    r = ops.rule_id(rule)
+    b = ops.trim_count(k) if rule == "trimmed" else 0
+    w_ref, out_ref = oracle.robust(peers, r, b, w=w)
+    wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate([to_dev(p, cuda) for p in peers], rule, w=wt, out=out, trim_b=b)
+    # median is pure selection: exact bits, NaN payload included
+    assert_bits_equal(host(out), out_ref, nan_equal=(rule != "median"), what=f"{rule} K={k}")
+    assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k}")
+
+
+@pytest.mark.parametrize("k,b", [(5, 0), (5, 2), (10, 3), (128, 0), (128, 63), (200, 10), (256, 51), (256, 100)])
+def test_trimmed_explicit_b(cuda, k, b):
+    n = 1000
+    peers = [oracle.synth(n, k + b, p, 1.0) for p in range(k)]
+    _, out_ref = oracle.robust(peers, 2, b)
+    out = ops.trimmed_mean([to_dev(p, cuda) for p in peers], trim_b=b)
+    assert_bits_equal(host(out), out_ref, what=f"trim K={k} b={b}")
+
+
+def test_robust_matches_torch_median(cuda):
+    """Independent pin for NaN-free data: torch.median's lower median."""
+    k, n = 64, 20000
+    x = torch.randn(k, n, generator=torch.Generator().manual_seed(3))
+    x[:, :100] = 0.0
+    got = ops.median([t.to(cuda).contiguous() for t in x])
+    assert torch.equal(got.cpu(), x.median(dim=0).values)
+
+
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+def test_dropin_robust_rules(cuda, rule, monkeypatch):
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
+    shapes = [("fc1.weight", (64, 33)), ("fc1.bias", (64,)), ("fc2.weight", (10, 64)), ("fc2.bias", (10,))]
+    n = sum(int(np.prod(s)) for _, s in shapes)
+    k = 9
+    peers = [oracle.synth(n, 11, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, 11, 0xFFFFF, 5e-2)
+    b = ops.trim_count(k)
+    w_ref, _ = oracle.robust(peers, ops.rule_id(rule), b, w=w)
+    model = Holder(shapes).to(cuda)
+    with torch.no_grad():
+        model.load_state_dict(split(w, shapes, cuda))
+    node = fake_node(model, [split(p, shapes, cuda) for p in peers])
+    agg.aggregate_models(node, rule=rule)
+    out = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+    assert_bits_equal(out, w_ref, what=f"dropin {rule}")
+
+
+# ------------------------------------------------------------------ SHA-256
+KATS = [
+    (b"", "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"),
+    (b"abc", "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"),
+    (b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq",
+     "248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"),
+    (b"a" * 1_000_000, "cdc76e5c9914fb9281a1c7e284d73e67f1809a48a497200e046d39ccc7112cd0"),
+]
+
+
+def test_sha256_kats(cuda):
+    got = ops.sha256_batch([m for m, _ in KATS])
+    assert [g.hex() for g in got] == [h for _, h in KATS]
+
+
+def test_sha256_lengths_and_alignment(cuda):
+    rng = np.random.default_rng(5)
+    lens = [0, 1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 129, 1000, 4095, 4096, 65537] + \
+        [int(x) for x in rng.integers(0, 20000, 100)]
+    msgs = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
+    assert ops.sha256_batch(msgs) == [hashlib.sha256(m).digest() for m in msgs]
+    # byte-offset (unaligned) messages inside one device buffer
+    hostbuf, offs, ls = ops.pack_messages(msgs[:40], align=1)
+    d = ops.sha256_batch_device(torch.from_numpy(hostbuf).to(cuda), offs, ls).cpu().numpy()
+    assert [bytes(d[i]) for i in range(40)] == [hashlib.sha256(m).digest() for m in msgs[:40]]
+
+
+def test_sha256_of_pickled_update(cuda):
+    """The exact bytes the reference signs: pickle.dumps(local_update) (node/node.py:285)."""
+    upd = {k: torch.randn(s, generator=torch.Generator().manual_seed(1))
+           for k, s in [("fc1.weight", (512, 784)), ("fc1.bias", (512,)), ("fc3.bias", (10,))]}
+    data = pickle.dumps(upd)
+    assert ops.sha256_batch([data])[0] == hashlib.sha256(data).digest() == oracle.sha256(data)
+
+
+def test_fused_digest_accept_fedavg(cuda):
+    """Digest K messages, reject corrupted ones, FedAvg the accepted in list order."""
+    k, n, hdr = 12, 10_000, 64
+    payloads = [oracle.synth(n, 21, p, 1e-2) for p in range(k)]
+    msgs = [bytes([p]) * hdr + payloads[p].tobytes() for p in range(k)]
+    expected = [hashlib.sha256(m).digest() for m in msgs]
+    bad = {2, 7, 8}
+    msgs = [m if p not in bad else m[:100] + bytes([m[100] ^ 1]) + m[101:] for p, m in enumerate(msgs)]
+    hostbuf, offs, ls = ops.pack_messages(msgs)
+    dbuf = torch.from_numpy(hostbuf).to(cuda)
+    dig = ops.sha256_batch_device(dbuf, offs, ls)
+    exp = torch.from_numpy(np.frombuffer(b"".join(expected), dtype=np.uint8).reshape(k, 32).copy()).to(cuda)
+    table = torch.tensor([dbuf.data_ptr() + o + hdr for o in offs], dtype=torch.int64, device=cuda)
+    accepted = torch.zeros(k, dtype=torch.int64, device=cuda)
+    count = torch.zeros(1, dtype=torch.int32, device=cuda)
+    ops.digest_accept(dig, exp, table, accepted, count)
+    w0 = oracle.synth(n, 21, 0xFFFFF, 5e-2)
+    wt = to_dev(w0, cuda)
+    ops.fedavg_apply_devk_(wt, accepted, count, k)
+    assert int(count.item()) == k - len(bad)
+    w_ref, _ = oracle.fedavg([payloads[p] for p in range(k) if p not in bad], w0)
+    assert_bits_equal(host(wt), w_ref, what="fused")
