@@ -1,0 +1,139 @@
+"""Coordinate sharding of the aggregation across the GPUs of one node.
+
+Every rule on the hot path is coordinate-wise (reference
+aggregator/aggregation.py:25-38 adds, divides and applies element by element),
+so the flat parameter vector shards by coordinate with no change to any
+output bit: each coordinate still sees all K peers in list order.
+  The one exchange step is an RCCL all-gather over xGMI
+that reassembles the global model.
+
+Ownership is ROUND-ROBIN BY CHUNK: with G ranks and chunk size C, global
+chunk c belongs to rank c % G.  Round s of rank g is global chunk s*G + g, so
+the all-gather of round s writes the contiguous global range
+[s*G*C, (s+1)*G*C) -- no scatter copies -- and round s's gather (on a comm
+stream) overlaps round s+1's reduction (on the compute stream).  The ragged
+tail (n not a multiple of G*C) is split evenly and gathered through a small
+staging buffer.
+
+Two data layouts use the same plan:
+  * replicated inputs (a tester holding every full update): ``sharded_aggregate_``
+    reads each rank's owned ranges in place from the full buffers;
+  * memory-sharded inputs (cfg3: 1.02 TB of updates never fit one GPU): each
+    rank holds only its owned coordinates (``ChunkPlan.local_len``), as in
+    bench.py, and gathers into the global model.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Sequence
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_CHUNK = 16 * 1024 * 1024  # coordinates per chunk (64 MB of fp32)
+
+
+@dataclass(frozen=True)
+class ChunkPlan:
+    n: int          # global coordinates
+    world: int
+    chunk: int
+
+    @property
+    def full_rounds(self) -> int:
+        return self.n // (self.world * self.chunk)
+
+    @property
+    def tail(self) -> int:
+        return self.n - self.full_rounds * self.world * self.chunk
+
+    @property
+    def tail_part(self) -> int:
+        return -(-self.tail // self.world) if self.tail else 0
+
+    def tail_range(self, rank: int):
+        """(global start, length) of this rank's piece of the ragged tail."""
+        base = self.full_rounds * self.world * self.chunk
+        lo = min(self.tail, rank * self.tail_part)
+        hi = min(self.tail, (rank + 1) * self.tail_part)
+        return base + lo, hi - lo
+
+    def owned(self, rank: int):
+        """List of (global start, length) this rank reduces, in round order."""
+        out = [((s * self.world + rank) * self.chunk, self.chunk) for s in range(self.full_rounds)]
+        if self.tail:
+            st, ln = self.tail_range(rank)
+            out.append((st, ln))
+        return out
+
+    def local_len(self, rank: int) -> int:
+        return sum(ln for _, ln in self.owned(rank))
+
+    def global_index(self, rank: int, i: int) -> int:
+        """Global coordinate of local element i (memory-sharded layout)."""
+        for st, ln in self.owned(rank):
+            if i < ln:
+                return st + i
+            i -= ln
+        raise IndexError(i)
+
+
+def _default_reduce(peers, w, rule, lr, trim_frac):
+    from . import ops
+
+    ops.aggregate(peers, rule, w=w, lr=lr, trim_frac=trim_frac)
+
+
+def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor], *, rule="fedavg",
+                       lr: float = 0.1, trim_frac: float = 0.2, chunk: int = DEFAULT_CHUNK,
+                       group=None, reduce: Callable | None = None, overlap: bool = True) -> ChunkPlan:
+    """w_full += lr * rule(peers) with the coordinates split across ranks.
+
+    Every rank holds the full w and the full peer buffers (replicated inputs);
+    each reduces its owned chunks in place, then all-gathers so every rank
+    ends with the identical global model -- byte-identical to one GPU.
+    ``reduce(peers, w, rule, lr, trim_frac)`` defaults to the HIP kernels;
+    tests substitute the CPU oracle to exercise the plan over gloo."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    n = w_full.numel()
+    plan = ChunkPlan(n, world, max(1, min(chunk, -(-n // world))))
+    reduce = reduce or _default_reduce
+    w = w_full.view(-1)
+    flat_peers = [p.reshape(-1) for p in peers_full]
+    on_gpu = w.is_cuda
+    comp = torch.cuda.current_stream(w.device) if on_gpu else None
+    comm = torch.cuda.Stream(w.device) if (on_gpu and overlap and world > 1) else None
+    C, G = plan.chunk, world
+    for s in range(plan.full_rounds):
+        st = (s * G + rank) * C
+        reduce([p[st:st + C] for p in flat_peers], w[st:st + C], rule, lr, trim_frac)
+        if world == 1:
+            continue
+        out = w[s * G * C:(s + 1) * G * C]
+        mine = w[st:st + C]
+        if comm is not None:
+            ev = torch.cuda.Event()
+            ev.record(comp)
+            comm.wait_event(ev)
+            with torch.cuda.stream(comm):
+                dist.all_gather_into_tensor(out, mine, group=group)
+        else:
+            dist.all_gather_into_tensor(out, mine.clone(), group=group)
+    if plan.tail:
+        st, ln = plan.tail_range(rank)
+        if ln:
+            reduce([p[st:st + ln] for p in flat_peers], w[st:st + ln], rule, lr, trim_frac)
+        if world > 1:
+            if comm is not None:
+                comp.wait_stream(comm)
+            part = plan.tail_part
+            stage = torch.zeros(part * G, dtype=w.dtype, device=w.device)
+            if ln:
+                stage[rank * part:rank * part + ln].copy_(w[st:st + ln])
+            dist.all_gather_into_tensor(stage, stage[rank * part:(rank + 1) * part].clone(), group=group)
+            base = plan.full_rounds * G * C
+            w[base:].copy_(stage[:plan.tail])
+    if comm is not None:
+        comp.wait_stream(comm)
+    return plan

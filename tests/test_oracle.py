@@ -1,0 +1,89 @@
+"""The oracle itself, pinned against the reference's golden vectors and KATs (CPU)."""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import assert_bits_equal, case_inputs, load_golden
+
+META, SMALL = load_golden()
+
+
+@pytest.mark.parametrize("case", META["cases"], ids=lambda c: c["name"])
+def test_c_and_numpy_oracles_match_reference_golden(case):
+    w, peers = case_inputs(case, SMALL)
+    for fn in (oracle.fedavg, oracle.fedavg_np):
+        out, _ = fn(peers, w, lr=case["lr"])
+        stride = case["sample_stride"]
+        want = np.array(case["sample_bits"], dtype=np.uint32).view(np.float32)
+        assert_bits_equal(out[::stride], want, what=f"{fn.__name__} {case['name']}")
+        if case["out_sha256"]:
+            assert hashlib.sha256(out.tobytes()).hexdigest() == case["out_sha256"]
+        if f"{case['name']}__out" in SMALL:
+            assert_bits_equal(out, SMALL[f"{case['name']}__out"])
+
+
+def test_golden_inputs_regenerate_from_numpy_prng():
+    """The golden inputs were made with oracle.synth_np; the C PRNG agrees."""
+    for case in META["cases"]:
+        if case["name"] == "special_k4":
+            continue
+        n = min(case["n"], 5000)
+        a = oracle.synth(n, case["seed"], 1, case["upd_scale"])
+        b = oracle.synth_np(n, case["seed"], 1, case["upd_scale"])
+        assert_bits_equal(a, b)
+
+
+def test_reference_error_behaviour_recorded():
+    b = META["behaviour"]
+    assert b["k0"] == {"returns": "None", "model_unchanged": True}
+    assert b["int_buffer"]["raises"] == "RuntimeError"
+    assert b["missing_key"]["raises"] == "KeyError"
+
+
+def test_sha256_kats_and_hashlib():
+    kats = {b"": "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855",
+            b"abc": "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad",
+            b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq":
+                "248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1",
+            b"a" * 1_000_000: "cdc76e5c9914fb9281a1c7e284d73e67f1809a48a497200e046d39ccc7112cd0"}
+    for m, h in kats.items():
+        assert oracle.sha256(m).hex() == h
+    rng = np.random.default_rng(0)
+    for L in [1, 55, 56, 63, 64, 65, 119, 120, 128, 1000, 70001]:
+        m = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        assert oracle.sha256(m) == hashlib.sha256(m).digest()
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 8, 33, 128, 256])
+def test_robust_oracles_agree(k):
+    n = 2000
+    peers = [oracle.synth(n, k, p, 1.0) for p in range(k)]
+    peers[0][:50] = np.nan
+    peers[-1][50:100] = -0.0
+    for rule, b in [(1, 0), (2, oracle.trim_count(k))]:
+        _, c = oracle.robust(peers, rule, b)
+        npv = oracle.robust_np(peers, rule, b)
+        assert_bits_equal(c, npv, nan_equal=(rule == 2), what=f"rule {rule} K={k}")
+
+
+def test_median_matches_torch_median_nan_free():
+    x = torch.randn(64, 5000, generator=torch.Generator().manual_seed(1))
+    x[:, :10] = 0.0
+    _, c = oracle.robust(list(x.numpy()), 1)
+    assert np.array_equal(c, x.median(dim=0).values.numpy())
+
+
+def test_trim_count():
+    assert [oracle.trim_count(k) for k in (1, 2, 4, 5, 9, 10, 128, 256)] == [0, 0, 0, 1, 1, 2, 25, 51]
+
+
+def test_sorting_networks_0_1_principle():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "p2pdl_amd", "csrc"))
+    import gen_networks
+
+    gen_networks.check()
