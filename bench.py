@@ -42,7 +42,13 @@ WORKLOADS = {
     "cfg2": ("fedavg", 64, 11_689_512, 0x5EED0001),
     "cfg4-median": ("median", 128, 100_000_000, 0x5EED0003),
     "cfg4-trimmed": ("trimmed", 128, 100_000_000, 0x5EED0003),
+    # cfg5: 256 serialized updates (64-B header + 25M fp32 payload), digest all,
+    # reject the ~10% whose bytes were corrupted, FedAvg the accepted ones
+    "cfg5": ("fused", 256, 25_000_000, 0x5EED0004),
+    # SHA-256 alone over 256 messages of the cfg5 size
+    "sha256": ("sha256", 256, 25_000_000, 0x5EED0004),
 }
+MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
 
 def log(*a):
@@ -64,6 +70,117 @@ def parse():
     return ap.parse_args()
 
 
+def run_digest_workload(args, rule, K, n, seed, dev):
+    """cfg5 / sha256: one process, one GPU (replicas only: see DESIGN.md)."""
+    import hashlib
+
+    import numpy as np
+
+    msg_bytes = MSG_HEADER + 4 * n
+    stride = -(-msg_bytes // 256) * 256
+    buf = torch.zeros(K * stride, dtype=torch.uint8, device=dev)
+    log(f"generating {K} messages x {msg_bytes:,} B ({K*stride/1e9:.1f} GB)")
+    for p in range(K):
+        hdr = np.frombuffer((f"p2pdl-update peer={p:05d} n={n} ".encode() + bytes(64))[:MSG_HEADER], dtype=np.uint8)
+        buf[p * stride:p * stride + MSG_HEADER].copy_(torch.from_numpy(hdr.copy()))
+        payload = buf[p * stride + MSG_HEADER:p * stride + msg_bytes].view(torch.float32)
+        ops.fill_synthetic_(payload, seed, p, UPD_SCALE)
+    offsets = [p * stride for p in range(K)]
+    lens = [msg_bytes] * K
+    ptrs = torch.tensor([buf.data_ptr() + o for o in offsets], dtype=torch.int64, device=dev)
+    lens_d = torch.tensor(lens, dtype=torch.int64, device=dev)
+    digests = torch.empty((K, 32), dtype=torch.uint8, device=dev)
+    lib = ops.N.lib()
+
+    def digest():
+        ops.N.check(lib.p2p_sha256_batch(ptrs.data_ptr(), lens_d.data_ptr(), K, digests.data_ptr(),
+                                         ops.N.stream_handle()), "sha256")
+
+    digest()
+    expected = digests.clone()  # what the senders signed (untimed)
+    torch.cuda.synchronize()
+    # cross-check two digests on the host (checker only)
+    for p in (0, K - 1):
+        assert bytes(digests[p].cpu().numpy()) == hashlib.sha256(
+            bytes(buf[offsets[p]:offsets[p] + msg_bytes].cpu().numpy())).digest(), "sha256 mismatch"
+    log("digest spot check vs hashlib: ok")
+    bad = [p for p in range(K) if (p * 7919) % 10 == 3]  # ~10% corrupted in flight
+    for p in bad:
+        buf[offsets[p] + MSG_HEADER + 1000] ^= 0x40
+    payload_tbl = torch.tensor([buf.data_ptr() + o + MSG_HEADER for o in offsets], dtype=torch.int64, device=dev)
+    accepted = torch.zeros(K, dtype=torch.int64, device=dev)
+    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    w = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.fill_synthetic_(w, seed, W_PEER, W_SCALE)
+    comp = torch.cuda.current_stream(dev)
+    kern = []
+
+    def step(record=False):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if record else None
+        if record:
+            e[0].record(comp)
+        digest()
+        if record:
+            e[1].record(comp)
+        if rule == "fused":
+            ops.digest_accept(digests, expected, payload_tbl, accepted, count)
+            ops.fedavg_apply_devk_(w, accepted, count, K)
+        if record:
+            e[2].record(comp)
+            kern.append(e)
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    if rule == "fused":
+        assert int(count.item()) == K - len(bad), "accept count"
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    step_s = el / args.steps
+    sha_ms = sum(a.elapsed_time(b) for a, b, _ in kern) / len(kern)
+    agg_ms = sum(b.elapsed_time(c) for _, b, c in kern) / len(kern)
+    hashed = K * msg_bytes
+    acc = K - len(bad)
+    agg_bytes = 4 * n * (acc + 2) if rule == "fused" else 0
+    cpu = None
+    if not args.no_cpu_baseline:
+        from concurrent.futures import ThreadPoolExecutor
+
+        thr = int(os.environ.get("OMP_NUM_THREADS", "16"))
+        sample = [bytes(buf[offsets[p]:offsets[p] + min(msg_bytes, 16 << 20)].cpu().numpy()) for p in range(min(K, 32))]
+        t0 = time.perf_counter()
+        reps = 0
+        with ThreadPoolExecutor(thr) as ex:  # hashlib releases the GIL
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                list(ex.map(lambda m: hashlib.sha256(m).digest(), sample))
+                reps += 1
+        ce = time.perf_counter() - t0
+        cpu = {"value": round(sum(map(len, sample)) * reps / ce / 1e9, 3), "unit": "GB/s", "cores": thr,
+               "kind": "port", "sample": f"hashlib.sha256 (OpenSSL, the function behind reference "
+                                         f"utils/crypto.py:56) over {len(sample)} x {len(sample[0]):,} B, "
+                                         f"{thr} threads, {reps} reps"}
+    line = {
+        "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
+        "value": round(hashed / step_s / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32 (SHA-256) + fp32",
+        "data": "synthetic serialized updates (64-B header + device-PRNG fp32 payload)",
+        "config": {"workload": f"{args.workload}: {K} messages x {msg_bytes:,} B"
+                               + (f", {len(bad)} corrupted, FedAvg over {acc} accepted" if rule == "fused" else ""),
+                   "peers": K, "coords_per_peer": n, "parallelism": "single GPU (replicas only)"},
+        "roofline": {"bound": "int-alu (serial SHA-256 chain per message; see DESIGN.md)",
+                     "achieved": round(hashed / (sha_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(hashed / (sha_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel_ms": round(sha_ms, 3), "fedavg_ms": round(agg_ms, 3),
+                     "fedavg_gbs": round(agg_bytes / (agg_ms / 1e3) / 1e9, 1) if agg_bytes else None},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -79,6 +196,10 @@ def main():
     rule, K, n, seed = WORKLOADS[args.workload]
     K = args.peers or K
     n = args.coords or n
+    if rule in ("fused", "sha256"):
+        if world > 1:
+            raise SystemExit("cfg5/sha256 run as replicas only (one process per GPU)")
+        return run_digest_workload(args, rule, K, n, seed, dev)
     S = args.chunks if world > 1 else 1
     C = -(-n // S)
     n = C * S  # whole chunks per rank

@@ -11,19 +11,22 @@
 // element once, keeps the running sum in VGPRs and touches w once:
 // algorithmic bytes = 4*n*(K+2) per launch (K peer reads + w read + w write).
 //
-// Layout: a lane owns kVec=8 consecutive floats (two 16-B dwordx4 loads per
-// peer); a 256-lane block owns a 2048-float tile.  The peer loop is unrolled
-// kUnroll deep so each lane keeps 2*kUnroll 16-B loads in flight.  Peer
-// streams are read once -> nontemporal loads.  No inter-block reuse exists,
-// so no XCD remap is needed (guide T1: 0% on elementwise).
+// Layout (measured, tools/fedavg_sweep.hip): a 256-lane block owns a
+// 4096-float tile; lane l owns the float4s at l, l+256, l+512, l+768 of it,
+// so EVERY load instruction reads one contiguous 1 KB per wave (a lane-
+// contiguous 32-B layout halves the useful bytes per instruction and ran at
+// 61-73% of peak).  The peer loop is unrolled 8 deep (32 x 16-B loads in
+// flight per lane), peer streams use nontemporal loads (read once), one tile
+// per block.  128 GB cfg3 tile: 6.18 TB/s = 77% of 8 TB/s.  No inter-block
+// reuse exists, so no XCD remap is needed (guide T1: 0% on elementwise).
 #include "p2p_common.h"
 
 namespace p2p {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kVec = 8;
-constexpr int kTile = kBlock * kVec;  // 2048 floats per tile
+constexpr int kNV = 4;                    // float4s per lane per tile
+constexpr int kTile = kBlock * 4 * kNV;   // 4096 floats per tile
 constexpr int kUnroll = 8;
 
 __device__ __forceinline__ f4 ld_nt(const float* p) {
@@ -52,56 +55,62 @@ __device__ __forceinline__ bool all_aligned16(const float* const* peers, int K, 
   return (m & 15) == 0;
 }
 
-// One tile, one lane's 8 elements starting at `base` (< n).
-__device__ __forceinline__ void fedavg_lane(const float* const* __restrict__ peers, int K,
-                                            int64_t n, int64_t base, float* w, float* out,
+// One tile starting at `tile0`; this lane's part.  Fast path: full tile and
+// 16-B aligned pointers.  Otherwise the same op order element by element.
+__device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ peers, int K,
+                                            int64_t n, int64_t tile0, float* w, float* out,
                                             float lr, bool aligned) {
   const float fk = static_cast<float>(K);
-  if (aligned && base + kVec <= n) {
-    f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
+  const int64_t base = tile0 + 4 * static_cast<int64_t>(threadIdx.x);
+  if (aligned && tile0 + kTile <= n) {
+    f4 acc[kNV];
+#pragma unroll
+    for (int v = 0; v < kNV; ++v) acc[v] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
     int k = 0;
     for (; k + kUnroll <= K; k += kUnroll) {
-      f4 x0[kUnroll], x1[kUnroll];
+      f4 x[kUnroll][kNV];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const float* p = peers[k + u] + base;
-        x0[u] = ld_nt(p);
-        x1[u] = ld_nt(p + 4);
+#pragma unroll
+        for (int v = 0; v < kNV; ++v) x[u][v] = ld_nt(p + kBlock * 4 * v);
       }
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {  // strictly in list order (:25-28)
-        a0 += x0[u];
-        a1 += x1[u];
-      }
+      for (int u = 0; u < kUnroll; ++u)  // strictly in list order (:25-28)
+#pragma unroll
+        for (int v = 0; v < kNV; ++v) acc[v] += x[u][v];
     }
     for (; k < K; ++k) {
       const float* p = peers[k] + base;
-      a0 += ld_nt(p);
-      a1 += ld_nt(p + 4);
+#pragma unroll
+      for (int v = 0; v < kNV; ++v) acc[v] += ld_nt(p + kBlock * 4 * v);
     }
-    const f4 m0 = div4(a0, fk), m1 = div4(a1, fk);  // (:31-32)
-    if (out) {
-      st(out + base, m0);
-      st(out + base + 4, m1);
-    }
-    if (w) {  // (:36-38)
-      st(w + base, apply4(ld(w + base), lr, m0));
-      st(w + base + 4, apply4(ld(w + base + 4), lr, m1));
+#pragma unroll
+    for (int v = 0; v < kNV; ++v) {
+      const int64_t o = base + kBlock * 4 * v;
+      const f4 m = div4(acc[v], fk);  // (:31-32)
+      if (out) st(out + o, m);
+      if (w) st(w + o, apply4(ld(w + o), lr, m));  // (:36-38)
     }
     return;
   }
-  // tail or unaligned: scalar path, same op order
-  const int cnt = static_cast<int>(n - base < kVec ? n - base : kVec);
-  for (int e = 0; e < cnt; ++e) {
-    float acc = 0.f;
-    for (int k = 0; k < K; ++k) acc += peers[k][base + e];
-    const float m = acc / fk;
-    if (out) out[base + e] = m;
-    if (w) w[base + e] = apply_lr(w[base + e], lr, m);
+  // partial tile or unaligned pointers: scalar path, same op order
+#pragma unroll 1
+  for (int v = 0; v < kNV; ++v) {
+#pragma unroll 1
+    for (int e = 0; e < 4; ++e) {
+      const int64_t i = base + kBlock * 4 * v + e;
+      if (i >= n) continue;
+      float acc = 0.f;
+      for (int k = 0; k < K; ++k) acc += peers[k][i];
+      const float m = acc / fk;
+      if (out) out[i] = m;
+      if (w) w[i] = apply_lr(w[i], lr, m);
+    }
   }
 }
 
-// Flat buffer, grid-stride over tiles.  K either from the kernarg or, when
+// Flat buffer, one tile per block.  K either from the kernarg or, when
 // k_dev != nullptr, from device memory (fused accept -> FedAvg path).
 __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const* __restrict__ peers,
                                                              int K, const int32_t* k_dev,
@@ -110,11 +119,7 @@ __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const*
   if (k_dev) K = *k_dev;
   if (K <= 0) return;
   const bool aligned = all_aligned16(peers, K, w, out);
-  const int64_t ntiles = ceil_div(n, kTile);
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int64_t base = t * kTile + static_cast<int64_t>(threadIdx.x) * kVec;
-    if (base < n) fedavg_lane(peers, K, n, base, w, out, lr, aligned);
-  }
+  fedavg_tile(peers, K, n, static_cast<int64_t>(blockIdx.x) * kTile, w, out, lr, aligned);
 }
 
 // Whole state_dict: one tile per block, segment found by binary search.
@@ -122,10 +127,8 @@ __global__ __launch_bounds__(kBlock) void fedavg_segments_kernel(const Seg* __re
                                                                  int nseg, int K, float lr) {
   const int64_t t = blockIdx.x;
   const Seg& s = segs[find_segment(segs, nseg, t)];
-  const int64_t base = (t - s.tile_begin) * kTile + static_cast<int64_t>(threadIdx.x) * kVec;
-  if (base >= s.n) return;
   const bool aligned = all_aligned16(s.peers, K, s.w, s.out);
-  fedavg_lane(s.peers, K, s.n, base, s.w, s.out, lr, aligned);
+  fedavg_tile(s.peers, K, s.n, (t - s.tile_begin) * kTile, s.w, s.out, lr, aligned);
 }
 
 __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* agg, float lr,
@@ -141,10 +144,11 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* ag
   }
 }
 
-static int grid_for_tiles(int64_t ntiles) {
-  // 256 CUs x 8 blocks of 256 lanes = full residency; grid-stride beyond.
-  const int64_t cap = 256 * 8;
-  return static_cast<int>(ntiles < cap ? (ntiles > 0 ? ntiles : 1) : cap);
+static int grid_for_tiles(int64_t ntiles) { return static_cast<int>(ntiles > 0 ? ntiles : 1); }
+
+static int grid_stride_blocks(int64_t nblocks) {
+  const int64_t cap = 256 * 8;  // 256 CUs x 8 resident blocks; grid-stride beyond
+  return static_cast<int>(nblocks < cap ? (nblocks > 0 ? nblocks : 1) : cap);
 }
 
 }  // namespace p2p
@@ -211,7 +215,7 @@ extern "C" int32_t p2p_apply_f32(float* w, const float* agg, float lr, int64_t n
   if (!w || !agg || n < 0) return P2P_ERR_INVALID;
   if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(agg)) & 3) return P2P_ERR_ALIGN;
   if (n == 0) return P2P_OK;
-  hipLaunchKernelGGL(apply_kernel, dim3(grid_for_tiles(ceil_div(n, kBlock * 4))), dim3(kBlock), 0,
+  hipLaunchKernelGGL(apply_kernel, dim3(grid_stride_blocks(ceil_div(n, kBlock * 4))), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), w, agg, lr, n);
   return launch_status();
 }

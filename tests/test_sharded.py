@@ -1,0 +1,93 @@
+"""Coordinate sharding + all-gather over gloo, world size 2, on CPU.
+
+The per-shard reduce is the CPU oracle injected through sharded_aggregate_'s
+``reduce`` seam (test-only); what is under test is the plan, the ragged tail,
+and that the gathered model is byte-identical to the unsharded result.  The
+GPU leg (same code with the HIP reduce and RCCL) runs in bench.py at N > 1.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from p2pdl_amd.sharded import ChunkPlan, sharded_aggregate_
+
+
+def test_chunk_plan_covers_every_coordinate_once():
+    for n, world, chunk in [(1000, 2, 64), (1000, 3, 7), (5, 4, 16), (4096, 8, 512), (1, 2, 1)]:
+        seen = np.zeros(n, dtype=int)
+        for r in range(world):
+            plan = ChunkPlan(n, world, chunk)
+            for st, ln in plan.owned(r):
+                seen[st:st + ln] += 1
+            assert plan.local_len(r) == sum(ln for _, ln in plan.owned(r))
+        assert (seen == 1).all(), (n, world, chunk)
+
+
+def test_global_index_matches_device_prng_mapping():
+    """Memory-sharded layout: local i -> global index == oracle.synth's chunk map."""
+    plan = ChunkPlan(8 * 4 * 100, 4, 100)
+    for r in range(4):
+        gi = [plan.global_index(r, i) for i in range(plan.local_len(r))]
+        a = oracle.synth(plan.local_len(r), 5, 1, 1.0, 100, 4, r)
+        b = oracle.synth(plan.n, 5, 1, 1.0)[gi]
+        assert np.array_equal(a, b)
+
+
+def oracle_reduce(peers, w, rule, lr, trim_frac):
+    rid = {"fedavg": 0, "median": 1, "trimmed": 2}[rule]
+    ps = [p.numpy() for p in peers]
+    if rid == 0:
+        new, _ = oracle.fedavg(ps, w.numpy(), lr=lr)
+    else:
+        new, _ = oracle.robust(ps, rid, oracle.trim_count(len(ps), trim_frac) if rid == 2 else 0,
+                               w=w.numpy(), lr=lr)
+    w.copy_(torch.from_numpy(new))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, n, k, rule, chunk, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        peers = [torch.from_numpy(oracle.synth(n, 17, p, 1e-2)) for p in range(k)]
+        w = torch.from_numpy(oracle.synth(n, 17, 0xFFFFF, 5e-2))
+        sharded_aggregate_(w, peers, rule=rule, chunk=chunk, reduce=oracle_reduce)
+        q.put((rank, w.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("rule,n,k,chunk", [("fedavg", 10_007, 5, 1000), ("fedavg", 4096, 3, 512),
+                                            ("median", 3001, 7, 256), ("trimmed", 777, 10, 100)])
+def test_gloo_world2_byte_identical_to_single(rule, n, k, chunk):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, k, rule, chunk, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    peers = [oracle.synth(n, 17, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, 17, 0xFFFFF, 5e-2)
+    if rule == "fedavg":
+        want, _ = oracle.fedavg(peers, w)
+    else:
+        rid = 1 if rule == "median" else 2
+        want, _ = oracle.robust(peers, rid, oracle.trim_count(k) if rid == 2 else 0, w=w)
+    assert got[0] == got[1] == want.tobytes()
