@@ -29,11 +29,9 @@ constexpr int kNV = 4;                    // float4s per lane per tile
 constexpr int kTile = kBlock * 4 * kNV;   // 4096 floats per tile
 constexpr int kUnroll = 8;
 
-__device__ __forceinline__ f4 ld_nt(const float* p) {
-  return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
-}
-__device__ __forceinline__ f4 ld(const float* p) { return *reinterpret_cast<const f4*>(p); }
-__device__ __forceinline__ void st(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+__device__ __forceinline__ f4 ld_nt(const float* p) { return ldg_nt(reinterpret_cast<const f4*>(p)); }
+__device__ __forceinline__ f4 ld(const float* p) { return ldg(reinterpret_cast<const f4*>(p)); }
+__device__ __forceinline__ void st(float* p, f4 v) { stg(reinterpret_cast<f4*>(p), v); }
 
 __device__ __forceinline__ f4 div4(f4 a, float k) {
   f4 r;
@@ -51,63 +49,94 @@ __device__ __forceinline__ f4 apply4(f4 w, float lr, f4 m) {
 __device__ __forceinline__ bool all_aligned16(const float* const* peers, int K, const float* w,
                                               const float* out) {
   uintptr_t m = reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(out);
-  for (int k = 0; k < K; ++k) m |= reinterpret_cast<uintptr_t>(peers[k]);
+  for (int k = 0; k < K; ++k) m |= reinterpret_cast<uintptr_t>(table_at(peers, k));
   return (m & 15) == 0;
 }
 
-// One tile starting at `tile0`; this lane's part.  Fast path: full tile and
-// 16-B aligned pointers.  Otherwise the same op order element by element.
+// One tile starting at `tile0`; this lane's part.  FULL: every float4 group
+// of the tile is in range (no predicates).  !FULL (the last, ragged tile):
+// complete float4 groups still use vector loads under a per-lane predicate;
+// the <= 3 trailing elements of the array go element by element.  Same op
+// order on every path.
+template <bool FULL>
+__device__ __forceinline__ void fedavg_tile_vec(const float* const* __restrict__ peers, int K,
+                                                int64_t n, int64_t base, float* w, float* out,
+                                                float lr) {
+  const float fk = static_cast<float>(K);
+  bool ok[kNV];
+#pragma unroll
+  for (int v = 0; v < kNV; ++v) ok[v] = FULL || (base + kBlock * 4 * v + 4 <= n);
+  f4 acc[kNV];
+#pragma unroll
+  for (int v = 0; v < kNV; ++v) acc[v] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
+  int k = 0;
+  for (; k + kUnroll <= K; k += kUnroll) {
+    f4 x[kUnroll][kNV];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const float* p = table_at(peers, k + u) + base;
+#pragma unroll
+      for (int v = 0; v < kNV; ++v)
+        x[u][v] = ok[v] ? ld_nt(p + kBlock * 4 * v) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)  // strictly in list order (:25-28)
+#pragma unroll
+      for (int v = 0; v < kNV; ++v) acc[v] += x[u][v];
+  }
+  for (; k < K; ++k) {
+    const float* p = table_at(peers, k) + base;
+#pragma unroll
+    for (int v = 0; v < kNV; ++v)
+      acc[v] += ok[v] ? ld_nt(p + kBlock * 4 * v) : f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int v = 0; v < kNV; ++v) {
+    if (!ok[v]) continue;
+    const int64_t o = base + kBlock * 4 * v;
+    const f4 m = div4(acc[v], fk);  // (:31-32)
+    if (out) st(out + o, m);
+    if (w) st(w + o, apply4(ld(w + o), lr, m));  // (:36-38)
+  }
+}
+
+// Element-wise path (misaligned views, and the < 4 trailing elements).
+__device__ __forceinline__ void fedavg_elem(const float* const* __restrict__ peers, int K, int64_t i,
+                                            float* w, float* out, float lr) {
+  float acc = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < K; ++k) acc += ldg(table_at(peers, k) + i);
+  const float m = acc / static_cast<float>(K);
+  if (out) stg(out + i, m);
+  if (w) stg(w + i, apply_lr(ldg(w + i), lr, m));
+}
+
 __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ peers, int K,
                                             int64_t n, int64_t tile0, float* w, float* out,
                                             float lr, bool aligned) {
-  const float fk = static_cast<float>(K);
   const int64_t base = tile0 + 4 * static_cast<int64_t>(threadIdx.x);
-  if (aligned && tile0 + kTile <= n) {
-    f4 acc[kNV];
-#pragma unroll
-    for (int v = 0; v < kNV; ++v) acc[v] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
-    int k = 0;
-    for (; k + kUnroll <= K; k += kUnroll) {
-      f4 x[kUnroll][kNV];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const float* p = peers[k + u] + base;
-#pragma unroll
-        for (int v = 0; v < kNV; ++v) x[u][v] = ld_nt(p + kBlock * 4 * v);
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u)  // strictly in list order (:25-28)
-#pragma unroll
-        for (int v = 0; v < kNV; ++v) acc[v] += x[u][v];
+  if (aligned) {
+    if (tile0 + kTile <= n) {
+      fedavg_tile_vec<true>(peers, K, n, base, w, out, lr);
+      return;
     }
-    for (; k < K; ++k) {
-      const float* p = peers[k] + base;
-#pragma unroll
-      for (int v = 0; v < kNV; ++v) acc[v] += ld_nt(p + kBlock * 4 * v);
-    }
-#pragma unroll
+    fedavg_tile_vec<false>(peers, K, n, base, w, out, lr);
+    // trailing elements of a float4 group that straddles n
+#pragma unroll 1
     for (int v = 0; v < kNV; ++v) {
-      const int64_t o = base + kBlock * 4 * v;
-      const f4 m = div4(acc[v], fk);  // (:31-32)
-      if (out) st(out + o, m);
-      if (w) st(w + o, apply4(ld(w + o), lr, m));  // (:36-38)
+      const int64_t g = base + kBlock * 4 * v;
+      if (g < n && g + 4 > n)
+        for (int64_t i = g; i < n; ++i) fedavg_elem(peers, K, i, w, out, lr);
     }
     return;
   }
-  // partial tile or unaligned pointers: scalar path, same op order
 #pragma unroll 1
-  for (int v = 0; v < kNV; ++v) {
+  for (int v = 0; v < kNV; ++v)
 #pragma unroll 1
     for (int e = 0; e < 4; ++e) {
       const int64_t i = base + kBlock * 4 * v + e;
-      if (i >= n) continue;
-      float acc = 0.f;
-      for (int k = 0; k < K; ++k) acc += peers[k][i];
-      const float m = acc / fk;
-      if (out) out[i] = m;
-      if (w) w[i] = apply_lr(w[i], lr, m);
+      if (i < n) fedavg_elem(peers, K, i, w, out, lr);
     }
-  }
 }
 
 // Flat buffer, one tile per block.  K either from the kernarg or, when
@@ -126,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const*
 __global__ __launch_bounds__(kBlock) void fedavg_segments_kernel(const Seg* __restrict__ segs,
                                                                  int nseg, int K, float lr) {
   const int64_t t = blockIdx.x;
-  const Seg& s = segs[find_segment(segs, nseg, t)];
+  const Seg s = load_segment(segs, nseg, t);
   const bool aligned = all_aligned16(s.peers, K, s.w, s.out);
   fedavg_tile(s.peers, K, s.n, (t - s.tile_begin) * kTile, s.w, s.out, lr, aligned);
 }
@@ -139,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* ag
     if (aligned && i + 4 <= n) {
       st(w + i, apply4(ld(w + i), lr, ld(agg + i)));
     } else {
-      for (int64_t j = i; j < n && j < i + 4; ++j) w[j] = apply_lr(w[j], lr, agg[j]);
+      for (int64_t j = i; j < n && j < i + 4; ++j) stg(w + j, apply_lr(ldg(w + j), lr, ldg(agg + j)));
     }
   }
 }

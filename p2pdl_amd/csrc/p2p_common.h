@@ -30,14 +30,58 @@ __device__ __forceinline__ float apply_lr(float w, float lr, float agg) {
   return __fadd_rn(w, __fmul_rn(lr, agg));
 }
 
-// Binary search of the segment owning tile `t` (segments sorted by tile_begin).
-__device__ __forceinline__ int find_segment(const Seg* segs, int nseg, int64_t t) {
+// Loads through the GLOBAL address space.  A generic pointer makes hipcc emit
+// flat_load, which also counts on lgkmcnt: every s_waitcnt lgkmcnt(0) for the
+// next scalar (pointer-table) load then drains all outstanding data loads.
+#define P2P_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ T ldg_nt(const T* p) {
+  return __builtin_nontemporal_load((const P2P_GLOBAL T*)(p));
+}
+template <typename T>
+__device__ __forceinline__ T ldg(const T* p) {
+  return *(const P2P_GLOBAL T*)(p);
+}
+template <typename T>
+__device__ __forceinline__ void stg(T* p, T v) {
+  *(P2P_GLOBAL T*)(p) = v;
+}
+
+// Entry k of a device pointer table, read through the CONSTANT address space
+// so a wave-uniform index becomes one scalar s_load (the table is read-only).
+#define P2P_CONST __attribute__((address_space(4)))
+template <typename T>
+__device__ __forceinline__ T* table_at(T* const* table, int k) {
+  return reinterpret_cast<T*>(((const P2P_CONST uint64_t*)(table))[k]);
+}
+
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// The descriptor of the segment owning tile `t` (segments sorted by
+// tile_begin), read through the scalar path: every field is forced
+// wave-uniform so the peer table and base pointers live in SGPRs and the
+// per-peer pointer loads are s_load, not per-lane vector loads.
+__device__ __forceinline__ Seg load_segment(const Seg* segs, int nseg, int64_t t) {
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (segs[mid].tile_begin <= t) lo = mid; else hi = mid - 1;
+    const int mid = (lo + hi + 1) >> 1;
+    const int64_t tb = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&segs[mid].tile_begin))));
+    if (tb <= t) lo = mid; else hi = mid - 1;
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
   }
-  return lo;
+  const Seg* sp = segs + lo;
+  Seg s;
+  s.peers = reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->peers))));
+  s.w = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->w))));
+  s.out = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->out))));
+  s.n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
+  s.tile_begin = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->tile_begin))));
+  return s;
 }
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

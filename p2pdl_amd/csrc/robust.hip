@@ -61,14 +61,16 @@ constexpr int kRobustTile = 128;  // coordinates per block (1 lane or a lane pai
 template <int KP, int RULE, int MODE>
 __device__ __forceinline__ float robust_coord(const float* const* __restrict__ peers, int K,
                                               int trim_b, int64_t i) {
+  // Loads are unconditional (a pad slot re-reads peer 0, an L2 hit) so the
+  // compiler can keep all of them in flight: a branch around each load made
+  // it wait for every load before the branch merge (serialised, ~8x slower).
   uint32_t v[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
-    if (j < K) {
-      v[j] = f2key(__float_as_uint(__builtin_nontemporal_load(peers[j] + i)));
-    } else {
-      v[j] = 0xFFFFFFFFu;  // pad: sorts after every real key
-    }
+    const bool real = (MODE != 0) || (j < K);  // MODE 1/2: K == KP
+    const float* p = table_at(peers, real ? j : 0);
+    const uint32_t key = f2key(__float_as_uint(ldg_nt(p + i)));
+    v[j] = real ? key : 0xFFFFFFFFu;  // pad: sorts after every real key
   }
   if constexpr (MODE == 0) {
     sort_full<KP>(v);
@@ -120,12 +122,12 @@ __device__ __forceinline__ float robust_coord_pair(const float* const* __restric
   const uint32_t m = h ? 0xFFFFFFFFu : 0u;
 #pragma unroll
   for (int j = 0; j < 128; ++j) {
-    const float* lo = peers[j];                           // K > 128: always valid
-    const float* hi = (128 + j < K) ? peers[128 + j] : lo;  // uniform guard
+    const float* lo = table_at(peers, j);                   // K > 128: always valid
+    const bool hi_real = (128 + j < K);
+    const float* hi = table_at(peers, hi_real ? 128 + j : j);  // uniform, no branch
     const float* p = h ? hi : lo;
-    uint32_t key = 0xFFFFFFFFu;
-    if (h == 0 || 128 + j < K) key = f2key(__float_as_uint(__builtin_nontemporal_load(p + i)));
-    v[j] = key ^ m;  // lane 1: complemented -> ascending sort = descending order
+    const uint32_t key = f2key(__float_as_uint(ldg_nt(p + i)));
+    v[j] = ((h == 0 || hi_real) ? key : 0xFFFFFFFFu) ^ m;  // lane 1: complemented
   }
   net_sort128(v);
 #pragma unroll
@@ -181,16 +183,16 @@ __device__ __forceinline__ void robust_one(const float* const* peers, int K, int
     const int64_t i = tile * kRobustTile + threadIdx.x;
     if (i >= n) return;
     const float agg = robust_coord<KP, RULE, MODE>(peers, K, trim_b, i);
-    if (out) out[i] = agg;
-    if (w) w[i] = apply_lr(w[i], lr, agg);
+    if (out) stg(out + i, agg);
+    if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
   } else {
     const int64_t i = tile * kRobustTile + (threadIdx.x >> 1);
     if (i >= n) return;  // both lanes of a pair leave together
     bool owner = false;
     const float agg = robust_coord_pair<RULE>(peers, K, trim_b, i, threadIdx.x & 1, &owner);
     if (owner) {
-      if (out) out[i] = agg;
-      if (w) w[i] = apply_lr(w[i], lr, agg);
+      if (out) stg(out + i, agg);
+      if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
     }
   }
 }
@@ -206,7 +208,7 @@ template <int KP, int RULE, int MODE>
 __global__ __launch_bounds__(KP <= 128 ? kRobustTile : 2 * kRobustTile) void robust_segments_kernel(
     const Seg* __restrict__ segs, int nseg, int K, int trim_b, float lr) {
   const int64_t t = blockIdx.x;
-  const Seg& s = segs[find_segment(segs, nseg, t)];
+  const Seg s = load_segment(segs, nseg, t);
   robust_one<KP, RULE, MODE>(s.peers, K, trim_b, s.n, t - s.tile_begin, s.w, s.out, lr);
 }
 

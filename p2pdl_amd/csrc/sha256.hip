@@ -23,6 +23,8 @@ __constant__ uint32_t kK256[64] = {
     0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int r) { return __builtin_rotateright32(x, r); }
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -55,7 +57,7 @@ __device__ __forceinline__ void compress(uint32_t (&h)[8], uint32_t (&W)[16]) {
 // full 64-B blocks are already consumed; `tail` points at the first tail byte.
 __device__ __forceinline__ uint32_t tail_byte(const uint8_t* tail, uint32_t rem, uint32_t j,
                                               uint32_t nblk, uint64_t bits) {
-  if (j < rem) return tail[j];
+  if (j < rem) return ldg(tail + j);
   if (j == rem) return 0x80u;
   const uint32_t end = 64u * nblk;
   if (j >= end - 8u) return static_cast<uint32_t>(bits >> (8u * (end - 1u - j))) & 0xFFu;
@@ -67,8 +69,8 @@ __global__ __launch_bounds__(64) void sha256_batch_kernel(const uint8_t* const* 
                                                           uint8_t* __restrict__ digests) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= k) return;
-  const uint8_t* m = msgs[i];
-  const uint64_t len = lens[i];
+  const uint8_t* m = ldg(msgs + i);
+  const uint64_t len = ldg(lens + i);
   uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                    0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
   const uint64_t full = len >> 6;
@@ -77,18 +79,18 @@ __global__ __launch_bounds__(64) void sha256_batch_kernel(const uint8_t* const* 
   for (uint64_t blk = 0; blk < full; ++blk) {
     const uint8_t* p = m + (blk << 6);
     if (al16) {
-      const uint4* q = reinterpret_cast<const uint4*>(p);
+      const u32x4* q = reinterpret_cast<const u32x4*>(p);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint4 x = q[j];
+        const u32x4 x = ldg(q + j);
         W[4 * j] = bswap(x.x); W[4 * j + 1] = bswap(x.y);
         W[4 * j + 2] = bswap(x.z); W[4 * j + 3] = bswap(x.w);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 16; ++j)
-        W[j] = (uint32_t(p[4 * j]) << 24) | (uint32_t(p[4 * j + 1]) << 16) |
-               (uint32_t(p[4 * j + 2]) << 8) | uint32_t(p[4 * j + 3]);
+        W[j] = (uint32_t(ldg(p + 4 * j)) << 24) | (uint32_t(ldg(p + 4 * j + 1)) << 16) |
+               (uint32_t(ldg(p + 4 * j + 2)) << 8) | uint32_t(ldg(p + 4 * j + 3));
     }
     compress(h, W);
   }
