@@ -42,6 +42,9 @@ WORKLOADS = {
     "cfg2": ("fedavg", 64, 11_689_512, 0x5EED0001),
     "cfg4-median": ("median", 128, 100_000_000, 0x5EED0003),
     "cfg4-trimmed": ("trimmed", 128, 100_000_000, 0x5EED0003),
+    # north-star robust target: median over 256 peers (cfg3's K) on a 100M tile
+    "median256": ("median", 256, 100_000_000, 0x5EED0005),
+    "trimmed256": ("trimmed", 256, 100_000_000, 0x5EED0005),
     # cfg5: 256 serialized updates (64-B header + 25M fp32 payload), digest all,
     # reject the ~10% whose bytes were corrupted, FedAvg the accepted ones
     "cfg5": ("fused", 256, 25_000_000, 0x5EED0004),
@@ -186,10 +189,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # P2P_DIST_BACKEND=gloo rehearses N>1 on a single GPU (ranks share cuda:0);
+    # the driver's multi-GPU runs use nccl (= RCCL over xGMI), one GPU per rank.
+    backend = os.environ.get("P2P_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -243,29 +253,35 @@ def main():
             comp.wait_stream(comm)
 
     # ---- correctness spot check of the first warmup step vs the oracle ----
-    check = None
-    if not args.no_check and rank == 0:
-        m = min(4096, C)
-        check = (w[:m].cpu().numpy().copy(), m)
+    # rank 0 checks the first m coordinates of EVERY rank's first chunk: in its
+    # own w and, at N > 1, where the all-gather placed them in the global model
+    m = min(4096, C)
+    check = not args.no_check and rank == 0
     for i in range(max(args.warmup, 1 if check else 0)):
         step()
-        if i == 0 and check is not None:
+        if i == 0 and check:
             torch.cuda.synchronize()
             import numpy as np
 
             import oracle  # checker only
-            w0, m = check
-            peers = [oracle.synth(m, seed, p, UPD_SCALE, C, world, rank) for p in range(K)]
             rid = ops.rule_id(rule)
-            if rid == 0:
-                want, _ = oracle.fedavg(peers, w0)
-            else:
-                want, _ = oracle.robust(peers, rid, ops.trim_count(K) if rid == 2 else 0, w=w0)
-            got = w[:m].cpu().numpy()
-            ok = np.array_equal(got.view(np.uint32), want.view(np.uint32))
-            log(f"[rank 0] spot check vs oracle ({m} coords): {'bit-exact' if ok else 'MISMATCH'}")
-            if not ok:
+            bad = []
+            for g in range(world):
+                peers = [oracle.synth(m, seed, p, UPD_SCALE, C, world, g) for p in range(K)]
+                w0 = oracle.synth(m, seed, W_PEER, W_SCALE, C, world, g)
+                if rid == 0:
+                    want, _ = oracle.fedavg(peers, w0)
+                else:
+                    want, _ = oracle.robust(peers, rid, ops.trim_count(K) if rid == 2 else 0, w=w0)
+                got = (w_full[g * C:g * C + m] if world > 1 else w[:m]).cpu().numpy()
+                if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                    bad.append(g)
+            log(f"[rank 0] spot check vs oracle ({m} coords x {world} rank chunk(s)): "
+                f"{'bit-exact' if not bad else f'MISMATCH on ranks {bad}'}")
+            if bad:
                 raise SystemExit("bench: kernel output differs from the oracle")
+        if world > 1:
+            dist.barrier()
 
     # ---- timed region ----
     if world > 1:

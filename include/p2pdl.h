@@ -51,15 +51,16 @@ typedef struct p2p_segment_t {
   float *w;                  /* model tensor for this key, updated in place (nullable) */
   float *out;                /* receives the aggregate before apply (nullable) */
   int64_t n;                 /* elements in this tensor */
-  int64_t tile_begin;        /* sum of ceil(n_j / p2p_tile_elems(rule)) over earlier segments */
+  int64_t tile_begin;        /* sum of ceil(n_j / p2p_tile_elems(rule, k)) over earlier segments */
 } p2p_segment_t;
 
 /* ABI version (P2P_ABI_VERSION) and error text (static storage). */
 int32_t p2p_abi_version(void);
 const char *p2p_strerror(int32_t code);
 
-/* Elements per tile of the segment kernel for `rule` (host planning helper). */
-int64_t p2p_tile_elems(int32_t rule);
+/* Elements per tile of the segment kernel for `rule` with k peers (host
+ * planning helper for p2p_segment_t.tile_begin). */
+int64_t p2p_tile_elems(int32_t rule, int32_t k);
 
 /* ---- K1: FedAvg --------------------------------------------------------
  * Replaces reference aggregator/aggregation.py:15-38 for one flat buffer:
@@ -91,7 +92,7 @@ int32_t p2p_aggregate_f32(const float *const *peers, int32_t k, int64_t n, int32
                           int32_t trim_b, float lr, float *w, float *out, p2p_stream_t stream);
 
 /* Whole state_dict in ONE launch: segs is a DEVICE array of nseg entries
- * (tile_begin prefix-summed with p2p_tile_elems(rule)); total_tiles is the
+ * (tile_begin prefix-summed with p2p_tile_elems(rule, k)); total_tiles is the
  * sum over all segments.  Replaces the per-key loops of
  * aggregator/aggregation.py:15,25-28,31-32,37-38. */
 int32_t p2p_aggregate_segments_f32(const p2p_segment_t *segs, int32_t nseg, int64_t total_tiles,

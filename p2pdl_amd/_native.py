@@ -43,7 +43,7 @@ _I32, _I64, _U64, _F32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes
 _SIGS = {
     "p2p_abi_version": ([], _I32),
     "p2p_strerror": ([_I32], ctypes.c_char_p),
-    "p2p_tile_elems": ([_I32], _I64),
+    "p2p_tile_elems": ([_I32, _I32], _I64),
     "p2p_fedavg_apply_f32": ([_P, _I32, _I64, _P, _F32, _P], _I32),
     "p2p_mean_f32": ([_P, _I32, _I64, _P, _P], _I32),
     "p2p_fedavg_apply_devk_f32": ([_P, _P, _I32, _I64, _P, _F32, _P, _P], _I32),

@@ -2,7 +2,7 @@
 #include "p2p_common.h"
 
 extern "C" int64_t p2p_fedavg_tile_elems(void);
-extern "C" int64_t p2p_robust_tile_elems(void);
+extern "C" int64_t p2p_robust_tile_elems(int32_t rule, int32_t k);
 extern "C" int32_t p2p_fedavg_segments_f32(const p2p_segment_t* segs, int32_t nseg,
                                            int64_t total_tiles, int32_t k, float lr,
                                            p2p_stream_t stream);
@@ -28,8 +28,8 @@ extern "C" const char* p2p_strerror(int32_t code) {
   return "p2p: unknown error";
 }
 
-extern "C" int64_t p2p_tile_elems(int32_t rule) {
-  return rule == P2P_RULE_FEDAVG ? p2p_fedavg_tile_elems() : p2p_robust_tile_elems();
+extern "C" int64_t p2p_tile_elems(int32_t rule, int32_t k) {
+  return rule == P2P_RULE_FEDAVG ? p2p_fedavg_tile_elems() : p2p_robust_tile_elems(rule, k);
 }
 
 static bool misaligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) != 0; }

@@ -8,42 +8,45 @@
 //            from +0, IEEE-divided by K-2b
 // followed by the same apply as FedAvg (aggregation.py:36-38).
 //
-// Design: one lane owns one coordinate.  Its K values are loaded (coalesced:
-// 64 lanes read 256 contiguous bytes of one peer per instruction), mapped to
-// uint32 total-order keys and sorted by a register-resident Batcher odd-even
-// merge network (networks.inc, generated and 0-1-principle checked by
-// gen_networks.py).  A compare-exchange is one v_min_u32 + one v_max_u32 on
-// VGPRs -- no LDS round trips per stage.  When K equals the padded size KP
-// and (for the trimmed mean) b = floor(0.2 K), a network pruned to the wanted
-// ranks is used (median128: 2299 VALU ops vs 2942 for the full sort).
-// Otherwise KP is the next power of two, slots K..KP-1 hold +inf pads
-// (0xFFFFFFFF keys sort last) and the rank is picked with predicated selects.
+// Keys: float bits mapped to uint32 so the total order is unsigned order;
+// a compare-exchange is one v_min_u32 + one v_max_u32 on VGPRs.  Networks are
+// Batcher odd-even merge sorts / bitonic mergers generated (and 0-1-principle
+// checked) by gen_networks.py into networks.inc.
 //
-// K in 129..256 runs on a LANE PAIR (256 live keys in one lane exceed the
-// 512-entry register file and stall the register allocator): lane h of the
-// pair holds peers [128h, 128h+128).  Lane 1 complements its keys so the same
-// ascending sort128 network leaves it DESCENDING; one cross-lane half-cleaner
-// (DPP quad_perm swap, min in lane 0 / max in lane 1) then puts the 128
-// smallest keys in lane 0 and the 128 largest in lane 1, both bitonic, and a
-// bmerge128 network sorts each lane.  The median of 256 is the max of lane 0
-// after the half-cleaner (no merge needed).
+// K <= 64: ONE LANE per coordinate (KP = next power of two, +inf pads; a
+// network pruned to the wanted ranks when K == 64).  Loads: each wave
+// instruction reads 256 contiguous bytes of one peer.
+//
+// K in 65..256: a WAVE GROUP per 64 coordinates -- P = 2 (K <= 128) or 4
+// waves, wave q holding peers [64q, 64q+64).  Each wave sorts its 64 keys in
+// registers (ascending or descending: bitonic block directions), then the
+// group runs a bitonic merge: cross-wave half-cleaners through LDS (16
+// registers per exchange round) and an in-register bmerge64.  ~75 VGPRs per
+// lane -> 6 waves/SIMD, where one lane holding 128 keys needs ~150 VGPRs
+// (3 waves/SIMD) and 256 keys do not fit.  The median of K = 64P stops after
+// the first half-cleaner of the final merge: the lower P/2 waves then hold the
+// K/2 smallest keys and the median is their maximum.  Trimmed sums run wave 0
+// -> wave P-1 in ascending rank order, handing the partial sum on through LDS.
+#include <stdlib.h>
+
 #include "p2p_common.h"
 
-#define P2P_CE(a, b)                     \
-  do {                                   \
-    const uint32_t lo_ = min((a), (b));  \
-    (b) = max((a), (b));                 \
-    (a) = lo_;                           \
-  } while (0)
-#define P2P_MIN(a, b) (a) = min((a), (b))
-#define P2P_MAX(a, b) (b) = max((a), (b))
-
 namespace p2p {
+
+template <bool ASC>
+__device__ __forceinline__ void ce(uint32_t& a, uint32_t& b) {
+  const uint32_t lo = min(a, b), hi = max(a, b);
+  if constexpr (ASC) { a = lo; b = hi; } else { a = hi; b = lo; }
+}
+#define P2P_CE(a, b) ce<ASC>((a), (b))
+#define P2P_MIN(a, b) (a) = (ASC ? min((a), (b)) : max((a), (b)))
+#define P2P_MAX(a, b) (b) = (ASC ? max((a), (b)) : min((a), (b)))
 #include "networks.inc"
 
-template <int KP> __device__ __forceinline__ void sort_full(uint32_t (&v)[KP]);
+template <int KP, bool ASC = true> __device__ __forceinline__ void sort_full(uint32_t (&v)[KP]);
 #define P2P_SORT(KP) \
-  template <> __device__ __forceinline__ void sort_full<KP>(uint32_t (&v)[KP]) { net_sort##KP(v); }
+  template <> __device__ __forceinline__ void sort_full<KP, true>(uint32_t (&v)[KP]) { net_sort##KP<true>(v); } \
+  template <> __device__ __forceinline__ void sort_full<KP, false>(uint32_t (&v)[KP]) { net_sort##KP<false>(v); }
 P2P_SORT(2) P2P_SORT(4) P2P_SORT(8) P2P_SORT(16) P2P_SORT(32) P2P_SORT(64) P2P_SORT(128)
 #undef P2P_SORT
 
@@ -51,12 +54,12 @@ P2P_SORT(2) P2P_SORT(4) P2P_SORT(8) P2P_SORT(16) P2P_SORT(32) P2P_SORT(64) P2P_S
 // MODE 1: pruned median network for K == KP;
 // MODE 2: pruned trimmed network for K == KP, b == floor(0.2 KP).
 template <int KP, int MODE> __device__ __forceinline__ void run_special(uint32_t (&v)[KP]);
-template <> __device__ __forceinline__ void run_special<64, 1>(uint32_t (&v)[64]) { net_median64(v); }
-template <> __device__ __forceinline__ void run_special<128, 1>(uint32_t (&v)[128]) { net_median128(v); }
-template <> __device__ __forceinline__ void run_special<64, 2>(uint32_t (&v)[64]) { net_trim64_b12(v); }
-template <> __device__ __forceinline__ void run_special<128, 2>(uint32_t (&v)[128]) { net_trim128_b25(v); }
+template <> __device__ __forceinline__ void run_special<64, 1>(uint32_t (&v)[64]) { net_median64<true>(v); }
+template <> __device__ __forceinline__ void run_special<128, 1>(uint32_t (&v)[128]) { net_median128<true>(v); }
+template <> __device__ __forceinline__ void run_special<64, 2>(uint32_t (&v)[64]) { net_trim64_b12<true>(v); }
+template <> __device__ __forceinline__ void run_special<128, 2>(uint32_t (&v)[128]) { net_trim128_b25<true>(v); }
 
-constexpr int kRobustTile = 128;  // coordinates per block (1 lane or a lane pair each)
+constexpr int kRobustTile = 128;  // coordinates per block (one lane each, or 2 groups of 64)
 
 template <int KP, int RULE, int MODE>
 __device__ __forceinline__ float robust_coord(const float* const* __restrict__ peers, int K,
@@ -69,8 +72,13 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
   for (int j = 0; j < KP; ++j) {
     const bool real = (MODE != 0) || (j < K);  // MODE 1/2: K == KP
     const float* p = table_at(peers, real ? j : 0);
-    const uint32_t key = f2key(__float_as_uint(ldg_nt(p + i)));
-    v[j] = real ? key : 0xFFFFFFFFu;  // pad: sorts after every real key
+    v[j] = __float_as_uint(ldg_nt(p + i));
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all KP loads in flight before the first use
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    const bool real = (MODE != 0) || (j < K);
+    v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pad: sorts after every real key
   }
   if constexpr (MODE == 0) {
     sort_full<KP>(v);
@@ -107,109 +115,263 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
   }
 }
 
-// ---- lane pair, K in 129..256 ---------------------------------------------
-__device__ __forceinline__ uint32_t pair_swap(uint32_t x) {
-  // DPP quad_perm [1,0,3,2]: exchange with the other lane of the pair
-  return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), 0xB1, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float pair_swapf(float x) { return __uint_as_float(pair_swap(__float_as_uint(x))); }
+// ---- wave group, K in 65..256 ----------------------------------------------
+// All-ascending bitonic merge across the P waves of a group: every wave sorts
+// its 64 keys ascending; merge stage `size` (waves per merged block) starts
+// with a FLIP (block position q against size-1-q, register j against the
+// partner's register 63-j), then plain half-cleaners at wave distances
+// size/4..1 (register j against j), then bmerge64 in registers.  No wave ever
+// sorts descending, so no wave-dependent network and no phi copies of v[].
+constexpr int kXchg = 16;  // registers exchanged through LDS per round
 
-// Returns the aggregate in the lane that owns it (*owner = true there).
-template <int RULE>
-__device__ __forceinline__ float robust_coord_pair(const float* const* __restrict__ peers, int K,
-                                                   int trim_b, int64_t i, int h, bool* owner) {
-  uint32_t v[128];
-  const uint32_t m = h ? 0xFFFFFFFFu : 0u;
+// LDS-only barrier: waits for this wave's LDS traffic, then s_barrier.  A
+// __syncthreads() would also wait vmcnt(0) and drain the register prefetch of
+// the next tile that is in flight during the sort.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ uint32_t keep(uint32_t a, uint32_t b, bool keep_min) {
+  const uint32_t lo = min(a, b), hi = max(a, b);
+  return keep_min ? lo : hi;  // keep_min is wave-uniform: one v_cndmask with an SGPR mask
+}
+
+// flip: v[j] = keep(v[j], partner.v[63-j]); rounds pair the low chunk
+// [8c, 8c+8) with the mirrored high chunk [56-8c, 64-8c).
+template <int H>
+__device__ __forceinline__ void xchg_flip(uint32_t (&v)[H], uint32_t* lds, int wave, int partner,
+                                          bool keep_min) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int j = 0; j < 128; ++j) {
-    const float* lo = table_at(peers, j);                   // K > 128: always valid
-    const bool hi_real = (128 + j < K);
-    const float* hi = table_at(peers, hi_real ? 128 + j : j);  // uniform, no branch
-    const float* p = h ? hi : lo;
-    const uint32_t key = f2key(__float_as_uint(ldg_nt(p + i)));
-    v[j] = ((h == 0 || hi_real) ? key : 0xFFFFFFFFu) ^ m;  // lane 1: complemented
-  }
-  net_sort128(v);
+  for (int c = 0; c < H / 16; ++c) {
 #pragma unroll
-  for (int j = 0; j < 128; ++j) {  // undo complement, then cross-lane half-cleaner
-    const uint32_t x = v[j] ^ m;
-    const uint32_t y = pair_swap(x);
-    v[j] = h ? max(x, y) : min(x, y);
+    for (int r = 0; r < 8; ++r) {
+      lds[(wave * kXchg + r) * 64 + lane] = v[8 * c + r];
+      lds[(wave * kXchg + 8 + r) * 64 + lane] = v[H - 1 - 8 * c - r];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      // partner's v[H-1-(8c+r)] sits in its high slot r; its v[8c+r] in low slot r
+      v[8 * c + r] = keep(v[8 * c + r], lds[(partner * kXchg + 8 + r) * 64 + lane], keep_min);
+      v[H - 1 - 8 * c - r] = keep(v[H - 1 - 8 * c - r], lds[(partner * kXchg + r) * 64 + lane], keep_min);
+    }
+    lds_barrier();
   }
+}
+
+// half-cleaner: v[j] = keep(v[j], partner.v[j])
+template <int H>
+__device__ __forceinline__ void xchg_half(uint32_t (&v)[H], uint32_t* lds, int wave, int partner,
+                                          bool keep_min) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < H; c += kXchg) {
+#pragma unroll
+    for (int r = 0; r < kXchg; ++r) lds[(wave * kXchg + r) * 64 + lane] = v[c + r];
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < kXchg; ++r) v[c + r] = keep(v[c + r], lds[(partner * kXchg + r) * 64 + lane], keep_min);
+    lds_barrier();
+  }
+}
+
+constexpr int kGroupTile = 64;  // coordinates per wave-group tile
+
+// Issue the 64 loads of one tile for this wave (raw float bits, no waits).
+template <int H, int MODE>
+__device__ __forceinline__ void group_issue(uint32_t (&nx)[H], const float* const* __restrict__ peers,
+                                            int K, int wi, int64_t ic) {
+#pragma unroll
+  for (int j = 0; j < H; ++j) {  // unconditional loads (pads re-read peer 0)
+    const int pj = wi * H + j;
+    nx[j] = __float_as_uint(ldg_nt(table_at(peers, (MODE == 1 || pj < K) ? pj : 0) + ic));
+  }
+  // keep the 64 loads back to back: under register pressure the scheduler
+  // otherwise pairs each load with its first use (64 serialised round trips)
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int H> __device__ __forceinline__ void sort_h(uint32_t (&v)[H]);
+template <> __device__ __forceinline__ void sort_h<64>(uint32_t (&v)[64]) { net_sort64<true>(v); }
+template <> __device__ __forceinline__ void sort_h<128>(uint32_t (&v)[128]) { net_sort128<true>(v); }
+template <int H> __device__ __forceinline__ void bmerge_h(uint32_t (&v)[H]);
+template <> __device__ __forceinline__ void bmerge_h<64>(uint32_t (&v)[64]) { net_bmerge64<true>(v); }
+
+
+// One 64-coordinate tile whose keys are in v[] (wave wi holds peers
+// [H*wi, H*wi+H)).  MODE 1: median with K == H*P (stops after the final flip).
+template <int H, int P, int RULE, int MODE>
+__device__ __forceinline__ void group_tile(uint32_t (&v)[H], int K, int trim_b, int wi, int lane,
+                                           int64_t i, bool live, float* w, float* out, float lr,
+                                           uint32_t* lds) {
+  sort_h<H>(v);
+  bool done = false;
+#pragma unroll
+  for (int size = 2; size <= P; size *= 2) {
+    const int q = wi % size, base = wi - q;
+    xchg_flip<H>(v, lds, wi, base + size - 1 - q, q < size / 2);
+    if constexpr (RULE == P2P_RULE_MEDIAN && MODE == 1) {
+      if (size == P) {  // lower P/2 waves now hold the K/2 smallest keys
+        uint32_t mx = v[0];
+#pragma unroll
+        for (int j = 1; j < H; ++j) mx = max(mx, v[j]);
+        if constexpr (P == 4) {  // combine waves 0 and 1
+          lds[wi * 64 + lane] = mx;
+          lds_barrier();
+          mx = max(mx, lds[(wi ^ 1) * 64 + lane]);
+          lds_barrier();
+        }
+        if (wi == 0 && live) {
+          const float agg = __uint_as_float(key2f(mx));
+          if (out) stg(out + i, agg);
+          if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
+        }
+        done = true;
+        break;
+      }
+    }
+#pragma unroll
+    for (int d = size / 4; d >= 1; d /= 2) xchg_half<H>(v, lds, wi, wi ^ d, (wi & d) == 0);
+    bmerge_h<H>(v);
+  }
+  if (done) return;
+  // fully sorted ascending across the group: wave wi holds ranks H*wi..H*wi+H-1
   if constexpr (RULE == P2P_RULE_MEDIAN) {
-    if (K == 256) {  // rank 127 = max of the lower half (lane 0)
-      uint32_t mx = v[0];
+    const int r = (K - 1) / 2;
+    if (wi == r / H) {
+      const int rl = r % H;
+      uint32_t sel = v[0];
 #pragma unroll
-      for (int j = 1; j < 128; ++j) mx = max(mx, v[j]);
-      *owner = (h == 0);
-      return __uint_as_float(key2f(mx));
+      for (int j = 1; j < H; ++j) sel = (j == rl) ? v[j] : sel;
+      if (live) {
+        const float agg = __uint_as_float(key2f(sel));
+        if (out) stg(out + i, agg);
+        if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
+      }
     }
-    net_bmerge128(v);
-    const int r = (K - 1) / 2;  // global rank; lane h holds ranks 128h..128h+127
-    const int rl = r - 128 * h;
-    uint32_t sel = v[0];
-#pragma unroll
-    for (int j = 1; j < 128; ++j) sel = (j == rl) ? v[j] : sel;
-    *owner = (rl >= 0 && rl < 128);
-    return __uint_as_float(key2f(sel));
   } else {
-    net_bmerge128(v);
+    float* part = reinterpret_cast<float*>(lds);  // partial-sum hand-off
     const int hi = K - trim_b;
-    float acc = 0.f;  // pass 1: lane 0 sums its ranks
+    float acc = 0.f;
+#pragma unroll 1
+    for (int qq = 0; qq < P; ++qq) {  // ascending rank order across the group
+      if (wi == qq) {
+        if (qq > 0) acc = part[lane];
 #pragma unroll
-    for (int j = 0; j < 128; ++j) {
-      const float s = __fadd_rn(acc, __uint_as_float(key2f(v[j])));
-      acc = (h == 0 && j >= trim_b && j < hi) ? s : acc;
+        for (int j = 0; j < H; ++j) {
+          const int g = qq * H + j;
+          const float s = __fadd_rn(acc, __uint_as_float(key2f(v[j])));
+          acc = (g >= trim_b && g < hi) ? s : acc;
+        }
+        part[lane] = acc;
+      }
+      lds_barrier();
     }
-    acc = pair_swapf(acc);  // lane 1 continues from lane 0's partial sum
-#pragma unroll
-    for (int j = 0; j < 128; ++j) {
-      const int g = 128 + j;
-      const float s = __fadd_rn(acc, __uint_as_float(key2f(v[j])));
-      acc = (h == 1 && g >= trim_b && g < hi) ? s : acc;
-    }
-    *owner = (h == 1);
-    return acc / static_cast<float>(K - 2 * trim_b);
-  }
-}
-
-// ---- kernels ---------------------------------------------------------------
-// KP <= 128: one lane per coordinate, 128-lane blocks.  KP == 256: lane pairs,
-// 256-lane blocks.  Either way a block covers kRobustTile coordinates.
-template <int KP, int RULE, int MODE>
-__device__ __forceinline__ void robust_one(const float* const* peers, int K, int trim_b, int64_t n,
-                                           int64_t tile, float* w, float* out, float lr) {
-  if constexpr (KP <= 128) {
-    const int64_t i = tile * kRobustTile + threadIdx.x;
-    if (i >= n) return;
-    const float agg = robust_coord<KP, RULE, MODE>(peers, K, trim_b, i);
-    if (out) stg(out + i, agg);
-    if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
-  } else {
-    const int64_t i = tile * kRobustTile + (threadIdx.x >> 1);
-    if (i >= n) return;  // both lanes of a pair leave together
-    bool owner = false;
-    const float agg = robust_coord_pair<RULE>(peers, K, trim_b, i, threadIdx.x & 1, &owner);
-    if (owner) {
+    if (wi == P - 1 && live) {
+      const float agg = acc / static_cast<float>(K - 2 * trim_b);
       if (out) stg(out + i, agg);
       if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
     }
   }
 }
 
+// Persistent wave group: block = P waves = one 64-coordinate tile at a time,
+// grid-stride over tiles, next tile's loads prefetched into registers while
+// the current tile is sorted and merged.
+template <int H, int P, int RULE, int MODE, bool SEGS, bool PREFETCH>
+__device__ __forceinline__ void robust_group_loop(const float* const* peers, const Seg* segs, int nseg,
+                                                  int64_t ntiles, int K, int trim_b, int64_t n, float* w,
+                                                  float* out, float lr, uint32_t* lds) {
+  const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  auto locate = [&](int64_t t, const float* const*& pp, int64_t& nn, float*& ww, float*& oo, int64_t& lt) {
+    if constexpr (SEGS) {
+      const Seg s = load_segment(segs, nseg, t);
+      pp = s.peers; nn = s.n; ww = s.w; oo = s.out; lt = t - s.tile_begin;
+    } else {
+      pp = peers; nn = n; ww = w; oo = out; lt = t;
+    }
+  };
+  int64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  const float* const* pp; int64_t nn; float* ww; float* oo; int64_t lt;
+  locate(t, pp, nn, ww, oo, lt);
+  uint32_t nx[H];
+  {
+    const int64_t i = lt * kGroupTile + lane;
+    group_issue<H, MODE>(nx, pp, K, wi, i < nn ? i : nn - 1);  // dead lanes re-read the last element
+  }
+  // PREFETCH: persistent grid-stride loop, next tile's loads in flight during
+  // the sort.  Otherwise one tile per block (grid = tiles).
+  const int64_t stride = PREFETCH ? static_cast<int64_t>(gridDim.x) : ntiles;
+  for (; t < ntiles; t += stride) {
+    const int64_t i = lt * kGroupTile + lane;
+    const bool live = i < nn;
+    float* cw = ww;
+    float* co = oo;
+    uint32_t v[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const uint32_t pad = (MODE == 1 || wi * H + j < K) ? 0u : 0xFFFFFFFFu;  // +inf pads sort last
+      v[j] = f2key(nx[j]) | pad;
+    }
+    if constexpr (PREFETCH) {
+      const int64_t tn = t + stride;
+      if (tn < ntiles) {  // prefetch the next tile (uniform branch)
+        locate(tn, pp, nn, ww, oo, lt);
+        const int64_t i2 = lt * kGroupTile + lane;
+        group_issue<H, MODE>(nx, pp, K, wi, i2 < nn ? i2 : nn - 1);
+      }
+    }
+    group_tile<H, P, RULE, MODE>(v, K, trim_b, wi, lane, i, live, cw, co, lr, lds);
+  }
+}
+
+// ---- kernels ---------------------------------------------------------------
+// KP <= 128 (template arg): one lane per coordinate, 128-lane blocks.
+// P in {2, 4} (GROUP kernels): 128*P-lane blocks.  A block covers kRobustTile
+// coordinates either way.
 template <int KP, int RULE, int MODE>
-__global__ __launch_bounds__(KP <= 128 ? kRobustTile : 2 * kRobustTile) void robust_flat_kernel(
+__device__ __forceinline__ void robust_one(const float* const* peers, int K, int trim_b, int64_t n,
+                                           int64_t tile, float* w, float* out, float lr) {
+  const int64_t i = tile * kRobustTile + threadIdx.x;
+  if (i >= n) return;
+  const float agg = robust_coord<KP, RULE, MODE>(peers, K, trim_b, i);
+  if (out) stg(out + i, agg);
+  if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
+}
+
+template <int KP, int RULE, int MODE>
+__global__ __launch_bounds__(kRobustTile) void robust_flat_kernel(
     const float* const* __restrict__ peers, int K, int trim_b, int64_t n, float* w, float* out,
     float lr) {
   robust_one<KP, RULE, MODE>(peers, K, trim_b, n, blockIdx.x, w, out, lr);
 }
 
 template <int KP, int RULE, int MODE>
-__global__ __launch_bounds__(KP <= 128 ? kRobustTile : 2 * kRobustTile) void robust_segments_kernel(
+__global__ __launch_bounds__(kRobustTile) void robust_segments_kernel(
     const Seg* __restrict__ segs, int nseg, int K, int trim_b, float lr) {
   const int64_t t = blockIdx.x;
   const Seg s = load_segment(segs, nseg, t);
   robust_one<KP, RULE, MODE>(s.peers, K, trim_b, s.n, t - s.tile_begin, s.w, s.out, lr);
+}
+
+template <int H, int P, int RULE, int MODE>
+__global__ __launch_bounds__(64 * P) void robust_group_flat_kernel(
+    const float* const* __restrict__ peers, int K, int trim_b, int64_t n, float* w, float* out,
+    float lr) {
+  __shared__ uint32_t lds[P * kXchg * 64];
+  robust_group_loop<H, P, RULE, MODE, false, (P == 4)>(peers, nullptr, 0, ceil_div(n, kGroupTile), K,
+                                                         trim_b, n, w, out, lr, lds);
+}
+
+template <int H, int P, int RULE, int MODE>
+__global__ __launch_bounds__(64 * P) void robust_group_segments_kernel(
+    const Seg* __restrict__ segs, int nseg, int64_t ntiles, int K, int trim_b, float lr) {
+  __shared__ uint32_t lds[P * kXchg * 64];
+  robust_group_loop<H, P, RULE, MODE, true, (P == 4)>(nullptr, segs, nseg, ntiles, K, trim_b, 0, nullptr,
+                                                        nullptr, lr, lds);
 }
 
 struct RobustArgs {
@@ -227,20 +389,35 @@ struct RobustArgs {
 
 template <int KP, int RULE, int MODE>
 static void launch_one(const RobustArgs& a) {
-  const dim3 block(KP <= 128 ? kRobustTile : 2 * kRobustTile);
   if (a.segs) {
     hipLaunchKernelGGL((robust_segments_kernel<KP, RULE, MODE>), dim3(static_cast<unsigned>(a.tiles)),
-                       block, 0, a.stream, a.segs, a.nseg, a.K, a.trim_b, a.lr);
+                       dim3(kRobustTile), 0, a.stream, a.segs, a.nseg, a.K, a.trim_b, a.lr);
   } else {
     hipLaunchKernelGGL((robust_flat_kernel<KP, RULE, MODE>),
-                       dim3(static_cast<unsigned>(ceil_div(a.n, kRobustTile))), block, 0, a.stream,
+                       dim3(static_cast<unsigned>(ceil_div(a.n, kRobustTile))), dim3(kRobustTile), 0,
+                       a.stream, a.peers, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
+  }
+}
+
+template <int H, int P, int RULE, int MODE>
+static void launch_group(const RobustArgs& a) {
+  const int64_t ntiles = a.segs ? a.tiles : ceil_div(a.n, kGroupTile);
+  // prefetching (P == 4) kernels are persistent: 2x the resident blocks
+  // (12 waves/CU); the others launch one block per tile
+  const int64_t cap = P == 4 ? 256 * (2 * 12 / P) : ntiles;
+  const unsigned grid = static_cast<unsigned>(ntiles < cap ? ntiles : cap);
+  if (a.segs) {
+    hipLaunchKernelGGL((robust_group_segments_kernel<H, P, RULE, MODE>), dim3(grid), dim3(64 * P), 0,
+                       a.stream, a.segs, a.nseg, a.tiles, a.K, a.trim_b, a.lr);
+  } else {
+    hipLaunchKernelGGL((robust_group_flat_kernel<H, P, RULE, MODE>), dim3(grid), dim3(64 * P), 0, a.stream,
                        a.peers, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
   }
 }
 
 template <int KP, int RULE>
 static void launch_kp(const RobustArgs& a) {
-  if constexpr (KP >= 64 && KP <= 128) {
+  if constexpr (KP == 64 || KP == 128) {
     if constexpr (RULE == P2P_RULE_MEDIAN) {
       if (a.K == KP) return launch_one<KP, RULE, 1>(a);
     } else {
@@ -250,6 +427,20 @@ static void launch_kp(const RobustArgs& a) {
   launch_one<KP, RULE, 0>(a);
 }
 
+template <int H, int P, int RULE>
+static void launch_p(const RobustArgs& a) {
+  if constexpr (RULE == P2P_RULE_MEDIAN) {
+    if (a.K == H * P) return launch_group<H, P, RULE, 1>(a);
+  }
+  launch_group<H, P, RULE, 0>(a);
+}
+
+// Layout per (rule, K), from measurements on MI355X:
+//   K <= 128     one lane per coordinate (median 68%, trimmed 56% of HBM peak
+//                at K = 128; a 2-wave x 64-key group reached 61%)
+//   K 129..256   4 waves x 64 keys with register prefetch of the next tile
+//                (median 42%, trimmed 25% at K = 256; 2 waves x 128 keys
+//                needs > 168 VGPRs and spills)
 template <int RULE>
 static void dispatch(const RobustArgs& a) {
   if (a.K <= 2) return launch_kp<2, RULE>(a);
@@ -259,7 +450,7 @@ static void dispatch(const RobustArgs& a) {
   if (a.K <= 32) return launch_kp<32, RULE>(a);
   if (a.K <= 64) return launch_kp<64, RULE>(a);
   if (a.K <= 128) return launch_kp<128, RULE>(a);
-  return launch_kp<256, RULE>(a);
+  return launch_p<64, 4, RULE>(a);
 }
 
 }  // namespace p2p
@@ -280,4 +471,7 @@ extern "C" P2P_INTERNAL int32_t p2p_robust_dispatch(const float* const* peers, c
   return e == hipSuccess ? P2P_OK : static_cast<int32_t>(e);
 }
 
-extern "C" P2P_INTERNAL int64_t p2p_robust_tile_elems(void) { return kRobustTile; }
+extern "C" P2P_INTERNAL int64_t p2p_robust_tile_elems(int32_t rule, int32_t k) {
+  (void)rule;
+  return k > 128 ? kGroupTile : kRobustTile;
+}

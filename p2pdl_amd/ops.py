@@ -163,7 +163,7 @@ def aggregate_segments_(ws: Sequence[torch.Tensor], peer_lists: Sequence[Sequenc
     if r != P2P_RULE_FEDAVG and K > MAX_ROBUST_PEERS:
         raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {K}")
     b = trim_count(K, trim_frac) if (r == P2P_RULE_TRIMMED and trim_b is None) else int(trim_b or 0)
-    tile = int(N.lib().p2p_tile_elems(r))
+    tile = int(N.lib().p2p_tile_elems(r, K))
     segs = np.zeros(L, dtype=_SEG_DTYPE)
     ptrs = np.zeros((L, K), dtype=np.uint64)
     tiles = 0

@@ -33,7 +33,8 @@ def test_abi_version_and_argument_errors_without_gpu():
     assert L.p2p_abi_version() == N.ABI_VERSION
     assert L.p2p_strerror(0) == b"ok"
     assert b"invalid" in L.p2p_strerror(-1)
-    assert L.p2p_tile_elems(0) == 4096 and L.p2p_tile_elems(1) == 128
+    assert L.p2p_tile_elems(0, 3) == 4096 and L.p2p_tile_elems(1, 64) == 128 and L.p2p_tile_elems(1, 200) == 64 \
+        and L.p2p_tile_elems(1, 128) == 128 and L.p2p_tile_elems(2, 129) == 64
     # argument validation happens before any HIP call
     assert L.p2p_fedavg_apply_f32(None, 3, 10, None, 0.1, None) == N.lib().p2p_aggregate_f32(
         None, 1, 1, 0, 0, 0.1, None, None, None) == -1

@@ -225,14 +225,14 @@ def test_robust_matches_torch_median(cuda):
 
 
 @pytest.mark.parametrize("rule", ["median", "trimmed"])
-def test_dropin_robust_rules(cuda, rule, monkeypatch):
+@pytest.mark.parametrize("k", [9, 64, 100, 128, 200, 256])
+def test_dropin_robust_rules(cuda, rule, k, monkeypatch):
     from p2pdl_amd.aggregator import aggregation as agg
 
     monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
     shapes = [("fc1.weight", (64, 33)), ("fc1.bias", (64,)), ("fc2.weight", (10, 64)), ("fc2.bias", (10,))]
     n = sum(int(np.prod(s)) for _, s in shapes)
-    k = 9
-    peers = [oracle.synth(n, 11, p, 1e-2) for p in range(k)]
+    peers = [oracle.synth(n, 11 + k, p, 1e-2) for p in range(k)]
     w = oracle.synth(n, 11, 0xFFFFF, 5e-2)
     b = ops.trim_count(k)
     w_ref, _ = oracle.robust(peers, ops.rule_id(rule), b, w=w)
