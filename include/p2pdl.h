@@ -99,6 +99,14 @@ int32_t p2p_aggregate_segments_f32(const p2p_segment_t *segs, int32_t nseg, int6
                                    int32_t k, int32_t rule, int32_t trim_b, float lr,
                                    p2p_stream_t stream);
 
+/* Tuning knob (process-wide, not thread-safe against concurrent launches):
+ * kernel layout for robust rules with 65 <= k <= 256.  0 = default (fastest
+ * measured per k), 1 = LDS-DMA staged 4 lanes per coordinate for every k,
+ * 2 = same with 2 lanes x 64 keys at k <= 128, 3 = the one-lane / 4-wave
+ * group kernels.  Results are identical; tile sizes (p2p_tile_elems) follow
+ * the layout, so segment tables must be built after choosing it. */
+int32_t p2p_set_robust_layout(int32_t layout);
+
 /* w += lr * agg, multiply and add separately rounded (aggregation.py:36-38). */
 int32_t p2p_apply_f32(float *w, const float *agg, float lr, int64_t n, p2p_stream_t stream);
 

@@ -45,14 +45,6 @@ __device__ __forceinline__ f4 apply4(f4 w, float lr, f4 m) {
   return r;
 }
 
-// Wave-uniform: are all peer pointers (and w/out) 16-B aligned?
-__device__ __forceinline__ bool all_aligned16(const float* const* peers, int K, const float* w,
-                                              const float* out) {
-  uintptr_t m = reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(out);
-  for (int k = 0; k < K; ++k) m |= reinterpret_cast<uintptr_t>(table_at(peers, k));
-  return (m & 15) == 0;
-}
-
 // One tile starting at `tile0`; this lane's part.  FULL: every float4 group
 // of the tile is in range (no predicates).  !FULL (the last, ragged tile):
 // complete float4 groups still use vector loads under a per-lane predicate;

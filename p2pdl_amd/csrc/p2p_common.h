@@ -17,11 +17,12 @@ using Seg = p2p_segment_t;
 
 // IEEE total order on float bits mapped to an unsigned key:
 // -NaN < -inf < ... < -0 < +0 < ... < +inf < +NaN.
+// Branch-free (arithmetic shift masks): 3 VALU ops, no VCC hazard s_nops.
 __device__ __forceinline__ uint32_t f2key(uint32_t b) {
-  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  return b ^ (static_cast<uint32_t>(static_cast<int32_t>(b) >> 31) | 0x80000000u);
 }
 __device__ __forceinline__ uint32_t key2f(uint32_t k) {
-  return (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+  return k ^ (~static_cast<uint32_t>(static_cast<int32_t>(k) >> 31) | 0x80000000u);
 }
 
 // w + lr*agg with the multiply and the add each rounded (no FMA), matching
@@ -82,6 +83,14 @@ __device__ __forceinline__ Seg load_segment(const Seg* segs, int nseg, int64_t t
   s.n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
   s.tile_begin = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->tile_begin))));
   return s;
+}
+
+// Wave-uniform: are all peer pointers (and w/out) 16-B aligned?
+__device__ __forceinline__ bool all_aligned16(const float* const* peers, int K, const float* w,
+                                              const float* out) {
+  uintptr_t m = reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(out);
+  for (int k = 0; k < K; ++k) m |= reinterpret_cast<uintptr_t>(table_at(peers, k));
+  return (m & 15) == 0;
 }
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -29,35 +29,9 @@
 // -> wave P-1 in ascending rank order, handing the partial sum on through LDS.
 #include <stdlib.h>
 
-#include "p2p_common.h"
+#include "robust_nets.h"
 
 namespace p2p {
-
-template <bool ASC>
-__device__ __forceinline__ void ce(uint32_t& a, uint32_t& b) {
-  const uint32_t lo = min(a, b), hi = max(a, b);
-  if constexpr (ASC) { a = lo; b = hi; } else { a = hi; b = lo; }
-}
-#define P2P_CE(a, b) ce<ASC>((a), (b))
-#define P2P_MIN(a, b) (a) = (ASC ? min((a), (b)) : max((a), (b)))
-#define P2P_MAX(a, b) (b) = (ASC ? max((a), (b)) : min((a), (b)))
-#include "networks.inc"
-
-template <int KP, bool ASC = true> __device__ __forceinline__ void sort_full(uint32_t (&v)[KP]);
-#define P2P_SORT(KP) \
-  template <> __device__ __forceinline__ void sort_full<KP, true>(uint32_t (&v)[KP]) { net_sort##KP<true>(v); } \
-  template <> __device__ __forceinline__ void sort_full<KP, false>(uint32_t (&v)[KP]) { net_sort##KP<false>(v); }
-P2P_SORT(2) P2P_SORT(4) P2P_SORT(8) P2P_SORT(16) P2P_SORT(32) P2P_SORT(64) P2P_SORT(128)
-#undef P2P_SORT
-
-// MODE 0: generic (full sort + runtime rank / trim);
-// MODE 1: pruned median network for K == KP;
-// MODE 2: pruned trimmed network for K == KP, b == floor(0.2 KP).
-template <int KP, int MODE> __device__ __forceinline__ void run_special(uint32_t (&v)[KP]);
-template <> __device__ __forceinline__ void run_special<64, 1>(uint32_t (&v)[64]) { net_median64<true>(v); }
-template <> __device__ __forceinline__ void run_special<128, 1>(uint32_t (&v)[128]) { net_median128<true>(v); }
-template <> __device__ __forceinline__ void run_special<64, 2>(uint32_t (&v)[64]) { net_trim64_b12<true>(v); }
-template <> __device__ __forceinline__ void run_special<128, 2>(uint32_t (&v)[128]) { net_trim128_b25<true>(v); }
 
 constexpr int kRobustTile = 128;  // coordinates per block (one lane each, or 2 groups of 64)
 
@@ -195,8 +169,6 @@ __device__ __forceinline__ void group_issue(uint32_t (&nx)[H], const float* cons
 template <int H> __device__ __forceinline__ void sort_h(uint32_t (&v)[H]);
 template <> __device__ __forceinline__ void sort_h<64>(uint32_t (&v)[64]) { net_sort64<true>(v); }
 template <> __device__ __forceinline__ void sort_h<128>(uint32_t (&v)[128]) { net_sort128<true>(v); }
-template <int H> __device__ __forceinline__ void bmerge_h(uint32_t (&v)[H]);
-template <> __device__ __forceinline__ void bmerge_h<64>(uint32_t (&v)[64]) { net_bmerge64<true>(v); }
 
 
 // One 64-coordinate tile whose keys are in v[] (wave wi holds peers
@@ -233,7 +205,7 @@ __device__ __forceinline__ void group_tile(uint32_t (&v)[H], int K, int trim_b, 
     }
 #pragma unroll
     for (int d = size / 4; d >= 1; d /= 2) xchg_half<H>(v, lds, wi, wi ^ d, (wi & d) == 0);
-    bmerge_h<H>(v);
+    bmerge<H>(v);
   }
   if (done) return;
   // fully sorted ascending across the group: wave wi holds ranks H*wi..H*wi+H-1
@@ -457,6 +429,45 @@ static void dispatch(const RobustArgs& a) {
 
 using namespace p2p;
 
+extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t k, int32_t variant);
+extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, const p2p_segment_t* segs,
+                                                   int32_t nseg, int64_t tiles, int32_t k, int32_t rule,
+                                                   int32_t trim_b, int64_t n, float* w, float* out, float lr,
+                                                   int32_t variant, p2p_stream_t stream);
+
+// Kernel family per K (tuning knob: p2p_set_robust_layout, or P2P_ROBUST_IMPL
+// in the environment, read on first use).  Results are identical; the
+// default is the fastest measured:
+//   0 "auto"   K <= 128: one lane per coordinate (this file);
+//              K 129..256: robust_lds.hip, 4 lanes x 64 keys
+//   1 "lds"    robust_lds.hip for every K in 65..256 (4 lanes x 32 keys at K <= 128)
+//   2 "lds2"   robust_lds.hip, 2 lanes x 64 keys at K <= 128
+//   3 "group"  this file only: one lane (K <= 128) / 4-wave LDS group (K > 128)
+static int g_robust_impl = -1;
+static int robust_impl() {
+  if (g_robust_impl < 0) {
+    const char* e = getenv("P2P_ROBUST_IMPL");
+    int v = 0;
+    if (e && e[0] == 'g') v = 3;
+    else if (e && e[0] == 'l' && e[1] == 'd' && e[2] == 's') v = (e[3] == '2') ? 2 : 1;
+    g_robust_impl = v;
+  }
+  return g_robust_impl;
+}
+
+// Which robust_lds.hip variant serves (k, impl), or -1 for this file's kernels.
+static int lds_variant(int k, int impl) {
+  if (k <= 64 || impl == 3) return -1;
+  if (k > 128) return 0;
+  return impl == 1 ? 0 : impl == 2 ? 1 : -1;
+}
+
+extern "C" int32_t p2p_set_robust_layout(int32_t layout) {
+  if (layout < 0 || layout > 3) return P2P_ERR_INVALID;
+  g_robust_impl = layout;
+  return P2P_OK;
+}
+
 extern "C" P2P_INTERNAL int32_t p2p_robust_dispatch(const float* const* peers, const p2p_segment_t* segs,
                                        int32_t nseg, int64_t tiles, int32_t k, int32_t rule,
                                        int32_t trim_b, int64_t n, float* w, float* out, float lr,
@@ -465,13 +476,20 @@ extern "C" P2P_INTERNAL int32_t p2p_robust_dispatch(const float* const* peers, c
   if (k > 256) return P2P_ERR_UNSUPPORTED;
   if (rule == P2P_RULE_TRIMMED && (trim_b < 0 || k - 2 * trim_b <= 0)) return P2P_ERR_INVALID;
   if (rule != P2P_RULE_MEDIAN && rule != P2P_RULE_TRIMMED) return P2P_ERR_INVALID;
-  RobustArgs a{peers, segs, nseg, tiles, k, trim_b, n, w, out, lr, static_cast<hipStream_t>(stream)};
-  if (rule == P2P_RULE_MEDIAN) dispatch<P2P_RULE_MEDIAN>(a); else dispatch<P2P_RULE_TRIMMED>(a);
+  const int var = lds_variant(k, robust_impl());
+  if (var >= 0) {
+    p2p_robust_lds_launch(peers, segs, nseg, tiles, k, rule, trim_b, n, w, out, lr, var, stream);
+  } else {
+    RobustArgs a{peers, segs, nseg, tiles, k, trim_b, n, w, out, lr, static_cast<hipStream_t>(stream)};
+    if (rule == P2P_RULE_MEDIAN) dispatch<P2P_RULE_MEDIAN>(a); else dispatch<P2P_RULE_TRIMMED>(a);
+  }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? P2P_OK : static_cast<int32_t>(e);
 }
 
 extern "C" P2P_INTERNAL int64_t p2p_robust_tile_elems(int32_t rule, int32_t k) {
   (void)rule;
+  const int var = lds_variant(k, robust_impl());
+  if (var >= 0) return p2p_robust_lds_tile(k, var);
   return k > 128 ? kGroupTile : kRobustTile;
 }

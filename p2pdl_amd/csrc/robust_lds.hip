@@ -1,0 +1,399 @@
+// K2 (K in 65..256) -- coordinate-wise median / trimmed mean with L lanes
+// per coordinate and the peer rows staged HBM -> LDS by LDS-DMA.
+//
+// Rule (no reference implementation, README.md:10):
+//   median : key of rank (K-1)/2 under the IEEE total order on float bits
+//   trimmed: b = floor(0.2 K); fp32 sum of ranks b..K-b-1 ascending from +0,
+//            IEEE-divided by K-2b
+// then w += lr*agg, multiply and add separately rounded (aggregation.py:36-38).
+//
+// Layout.  A block of L waves owns a tile of 64 coordinates; wave wi takes
+// coordinates [16*wi*4/L ...) -- 64/L of them -- and lane = L*c + q holds
+// keys q*H .. q*H+H-1 (H = KP/L) of coordinate c, so every cross-lane step
+// is a DPP quad_perm inside a quad, never LDS.  Each lane sorts its H keys
+// in VGPRs (Batcher network), then the L slices are merged bitonically:
+// stage s (2, 4 lanes) = a FLIP against lane q^(s-1) (register j vs the
+// partner's H-1-j), half-cleaners against q^d, and an in-register bitonic
+// merge.  A keep-min / keep-max against the partner is ONE v_med3_u32 with a
+// lane-constant 0 / ~0 third operand (plus the DPP move).
+//
+// Staging.  The block's LDS image holds its tile as L slices of H rows x 64
+// floats (row = one peer, 256 contiguous bytes in HBM) plus the w row.  The
+// next tile's rows are requested with global_load_lds_dwordx4 (1 KiB = 4
+// rows per wave-instruction, no VGPR destination, the L waves split the
+// pieces) as soon as the current tile has been read into registers, so the
+// HBM latency hides behind the sort and the register file holds one tile.
+// Two barriers per tile: after the DMA lands (vmcnt(0) + s_barrier) and after
+// the image is read (lgkmcnt(0) + s_barrier) before it is overwritten.
+// Slices are padded by 128/L bytes so the L lanes of a coordinate hit
+// different banks.  Measured: per-wave tiles with 64-B rows (16 coordinates)
+// ran 34% of HBM peak at K = 256 -- 256-B rows per peer are what the HBM
+// side needs (FedAvg reads 1 KiB runs).
+//
+// XCD placement: logical block g = (blockIdx % 8) * (grid / 8) + blockIdx / 8,
+// so neighbouring tiles are read through the same XCD's L2.
+//
+// Tiles that cannot be DMA'd (a peer / w pointer not 16-B aligned, or the
+// ragged last tile of a buffer) load the same keys with per-lane global
+// loads; the arithmetic after the load is the same code.
+#include "robust_nets.h"
+
+#define P2P_LDS __attribute__((address_space(3)))
+
+namespace p2p {
+
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  return max(min(a, b), min(max(a, b), c));  // -> v_med3_u32
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, 0xF, 0xF, false));
+}
+// value of lane (lane ^ M) inside the quad
+template <int M>
+__device__ __forceinline__ uint32_t xq(uint32_t x) {
+  static_assert(M >= 1 && M <= 3, "quad partner");
+  return dpp<M == 1 ? 0xB1 : (M == 2 ? 0x4E : 0x1B)>(x);
+}
+// value of slice q-1 of the same coordinate (slice 0 receives its own)
+template <int L>
+__device__ __forceinline__ float from_prev_slice(float x) {
+  static_assert(L == 2 || L == 4, "lanes per coordinate");
+  return __uint_as_float(dpp<L == 4 ? 0x90 : 0xA0>(__float_as_uint(x)));
+}
+
+template <int L, int H>
+struct LdsLayout {
+  static constexpr int W = L;                  // waves per block
+  static constexpr int TB = 64;                // coordinates per block tile
+  static constexpr int TW = TB / W;            // coordinates per wave (= lanes / L)
+  static constexpr int RB = 4 * TB;            // bytes per peer row (256 contiguous in HBM)
+  static constexpr int PAD = L > 1 ? 128 / L : 0;
+  static constexpr int SB = H * RB + PAD;      // bytes per slice
+  static constexpr int WOFF = L * SB;          // w row
+  static constexpr int BYTES = WOFF + RB;
+  static constexpr int CPS = H * RB / 1024;    // 1 KiB DMA pieces per slice (4 rows each)
+  static constexpr int NCHW = CPS * L / W;     // DMA pieces per wave per tile
+  static_assert((H * RB) % 1024 == 0 && NCHW * W == CPS * L, "slice must be whole 1 KiB DMA pieces");
+};
+
+__device__ __forceinline__ void glds16(const float* src, uint8_t P2P_LDS* dst) {
+  __builtin_amdgcn_global_load_lds((P2P_GLOBAL void*)(const_cast<float*>(src)), (P2P_LDS void*)dst, 16, 0, 0);
+}
+
+// Where a tile lives (flat buffer or one segment of a state_dict).
+struct TileSrc {
+  const float* const* peers;
+  float* w;
+  float* out;
+  int64_t n;
+  int64_t c0;   // first coordinate of the tile inside the buffer
+  int64_t seg;  // identity of the source (its first tile) for the pointer cache
+};
+
+template <int TW, bool SEGS>
+__device__ __forceinline__ TileSrc locate(const float* const* peers, const Seg* segs, int nseg, int64_t n,
+                                          float* w, float* out, int64_t t) {
+  if constexpr (SEGS) {
+    const Seg s = load_segment(segs, nseg, t);
+    return TileSrc{s.peers, s.w, s.out, s.n, (t - s.tile_begin) * TW, s.tile_begin};
+  } else {
+    return TileSrc{peers, w, out, n, t * TW, 0};
+  }
+}
+
+// The L-lane reduction of one coordinate.  v[] holds this lane's H keys
+// (pads = 0xFFFFFFFF); returns the aggregate, valid in the lane where
+// `own` is set on return.
+template <int L, int H, int RULE, int MODE>
+__device__ __forceinline__ float reduce_keys(uint32_t (&v)[H], int q, int K, int trim_b, bool& own) {
+  static_assert(L == 1 || L == 2 || L == 4, "lanes per coordinate");
+  if constexpr (L == 1) {
+    if constexpr (MODE == 0) sort_full<H>(v); else run_special<H, MODE>(v);
+    own = true;
+    if constexpr (RULE == P2P_RULE_MEDIAN) {
+      if constexpr (MODE == 1) return __uint_as_float(key2f(v[(H - 1) / 2]));
+      const int r = (K - 1) / 2;
+      uint32_t sel = v[0];
+#pragma unroll
+      for (int j = 1; j < H; ++j) sel = (j == r) ? v[j] : sel;
+      return __uint_as_float(key2f(sel));
+    } else {
+      float acc = 0.f;
+      if constexpr (MODE == 2) {
+        constexpr int b = (H * 2) / 10;
+#pragma unroll
+        for (int j = b; j < H - b; ++j) acc = __fadd_rn(acc, __uint_as_float(key2f(v[j])));
+        return acc / static_cast<float>(H - 2 * b);
+      }
+      const int hi = K - trim_b;
+#pragma unroll
+      for (int j = 0; j < H; ++j)
+        if (j >= trim_b && j < hi) acc = __fadd_rn(acc, __uint_as_float(key2f(v[j])));  // uniform predicate
+      return acc / static_cast<float>(K - 2 * trim_b);
+    }
+  } else {
+    sort_full<H>(v);
+#pragma unroll
+    for (int s = 2; s <= L; s *= 2) {
+      {  // flip against the mirrored lane of the s-lane group
+        const uint32_t keep = (q & (s / 2)) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+        for (int j = 0; j < H / 2; ++j) {
+          const uint32_t a = v[j], b = v[H - 1 - j];
+          const uint32_t pa = (s == 2) ? xq<1>(b) : xq<3>(b);  // partner's v[H-1-j]
+          const uint32_t pb = (s == 2) ? xq<1>(a) : xq<3>(a);  // partner's v[j]
+          v[j] = umed3(a, pa, keep);
+          v[H - 1 - j] = umed3(b, pb, keep);
+        }
+      }
+      if constexpr (RULE == P2P_RULE_MEDIAN && MODE == 1) {
+        if (s == L) {  // slices q < L/2 now hold the K/2 smallest keys; median = their max
+          uint32_t mx = v[0];
+#pragma unroll
+          for (int j = 1; j < H; ++j) mx = max(mx, v[j]);
+          if constexpr (L == 4) mx = max(mx, xq<1>(mx));
+          own = (q == 0);
+          return __uint_as_float(key2f(mx));
+        }
+      }
+#pragma unroll
+      for (int d = s / 4; d >= 1; d /= 2) {  // half-cleaners (only at s = 4: d = 1)
+        const uint32_t keep = (q & d) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+        for (int j = 0; j < H; ++j) v[j] = umed3(v[j], xq<1>(v[j]), keep);
+      }
+      bmerge<H>(v);
+    }
+    // slice q now holds ranks q*H .. q*H+H-1, ascending
+    if constexpr (RULE == P2P_RULE_MEDIAN) {
+      const int r = (K - 1) / 2;
+      const int rl = r % H;
+      uint32_t sel = v[0];
+#pragma unroll
+      for (int j = 1; j < H; ++j) sel = (j == rl) ? v[j] : sel;
+      own = (q == r / H);
+      return __uint_as_float(key2f(sel));
+    } else {
+      // ascending-rank sequential sum from +0: slice 0's ranks, then slice 1 ...
+      constexpr int KP = L * H;
+      const int b = MODE == 2 ? (KP * 2) / 10 : trim_b;
+      const int hi = MODE == 2 ? KP - b : K - trim_b;
+      if constexpr (MODE == 2) {  // once: a key is summed in up to L phases
+#pragma unroll
+        for (int j = 0; j < H; ++j) v[j] = key2f(v[j]);
+      }
+      float acc = 0.f;
+#pragma unroll
+      for (int p = 0; p < L; ++p) {
+        float a = p == 0 ? 0.f : from_prev_slice<L>(acc);
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+          const int g = p * H + j;
+          if (g >= b && g < hi)  // wave-uniform
+            a = __fadd_rn(a, __uint_as_float(MODE == 2 ? v[j] : key2f(v[j])));
+        }
+        acc = (q == p) ? a : acc;
+      }
+      own = (q == L - 1);
+      return acc / static_cast<float>(MODE == 2 ? KP - 2 * b : K - 2 * trim_b);
+    }
+  }
+}
+
+// Register-staged fill of the LDS image for a tile that cannot be DMA'd
+// (misaligned pointer or ragged tail): each lane writes exactly the words it
+// reads back.  Out of line: its row-pointer loads must not share the
+// register budget of the sorting loop.
+template <int L, int H>
+__device__ __attribute__((noinline)) void fill_direct(uint8_t P2P_LDS* lds, const float* const* tbl,
+                                                      const float* w, int64_t n, int64_t i, int K, int q,
+                                                      int c) {
+  using Lay = LdsLayout<L, H>;
+  const int64_t ic = i < n ? i : n - 1;  // dead lanes re-read the last element
+  uint32_t P2P_LDS* sl = (uint32_t P2P_LDS*)(lds + q * Lay::SB) + c;
+#pragma unroll
+  for (int j0 = 0; j0 < H; j0 += 16) {
+    uint32_t x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int row = q * H + j0 + j;
+      x[j] = __float_as_uint(ldg(table_at(tbl, row < K ? row : K - 1) + ic));
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sl[(j0 + j) * (Lay::RB / 4)] = x[j];
+  }
+  if (w && q == 0) ((float P2P_LDS*)(lds + Lay::WOFF))[c] = ldg(w + ic);
+}
+
+__device__ __forceinline__ void block_sync_vm() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void block_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int L, int H, int RULE, int MODE, bool SEGS>
+__global__ __launch_bounds__(64 * L) void robust_lds_kernel(const float* const* __restrict__ peers,
+                                                            const Seg* __restrict__ segs, int nseg,
+                                                            int64_t ntiles, int K, int trim_b, int64_t n,
+                                                            float* w, float* out, float lr) {
+  using Lay = LdsLayout<L, H>;
+  __shared__ __attribute__((aligned(16))) uint8_t lds_raw[Lay::BYTES];
+  uint8_t P2P_LDS* lds = (uint8_t P2P_LDS*)lds_raw;
+  const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int q = lane % L, c = wi * Lay::TW + lane / L;  // c: coordinate inside the block tile
+
+  const int64_t nb = gridDim.x;
+  int64_t t = blockIdx.x;
+  if ((nb & 7) == 0) t = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);  // XCD-contiguous tiles
+  if (t >= ntiles) return;
+
+  // per-lane row pointers of this wave's DMA pieces for the current source
+  const float* rp[Lay::NCHW];
+  int64_t cur_seg = -1;
+  bool aligned = false;
+  auto bind = [&](const TileSrc& s) {
+    if (s.seg == cur_seg) return;
+    cur_seg = s.seg;
+    aligned = all_aligned16(s.peers, K, s.w, nullptr);
+#pragma unroll
+    for (int m = 0; m < Lay::NCHW; ++m) {
+      const int ch = wi * Lay::NCHW + m;
+      const int row = (ch / Lay::CPS) * H + (ch % Lay::CPS) * 4 + lane / 16;
+      rp[m] = table_at(s.peers, row < K ? row : K - 1);
+    }
+  };
+  auto dma_ok = [&](const TileSrc& s) { return aligned && s.c0 + Lay::TB <= s.n; };
+  auto issue = [&](const TileSrc& s) {
+    const int64_t off = s.c0 + 4 * (lane % 16);
+#pragma unroll
+    for (int m = 0; m < Lay::NCHW; ++m) {
+      const int ch = wi * Lay::NCHW + m;
+      const int row0 = (ch / Lay::CPS) * H + (ch % Lay::CPS) * 4;
+      if (MODE != 0 || row0 < K)  // wave-uniform: pieces made only of pad rows are skipped
+        glds16(rp[m] + off, lds + (ch / Lay::CPS) * Lay::SB + (ch % Lay::CPS) * 1024);
+    }
+    if (s.w && wi == 0 && lane < 16) glds16(s.w + s.c0 + 4 * lane, lds + Lay::WOFF);
+  };
+
+  TileSrc cur = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t);
+  bind(cur);
+  bool dma_cur = dma_ok(cur);
+  if (dma_cur) issue(cur);
+
+  for (; t < ntiles; t += nb) {
+    const int64_t i = cur.c0 + c;
+    if (!dma_cur) fill_direct<L, H>(lds, cur.peers, cur.w, cur.n, i, K, q, c);
+    block_sync_vm();  // every wave's DMA pieces have landed
+    uint32_t v[H];
+    {
+      const uint32_t P2P_LDS* sl = (const uint32_t P2P_LDS*)(lds + q * Lay::SB) + c;
+#pragma unroll
+      for (int j = 0; j < H; ++j) v[j] = sl[j * (Lay::RB / 4)];
+    }
+    const float wv = cur.w ? ((const float P2P_LDS*)(lds + Lay::WOFF))[c] : 0.f;
+    block_sync_lds();  // image consumed: free for the next tile's DMA
+    // prefetch the next tile of this block while this one is sorted
+    const TileSrc nxt = (t + nb < ntiles) ? locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t + nb) : cur;
+    bool dma_nxt = false;
+    if (t + nb < ntiles) {
+      bind(nxt);
+      dma_nxt = dma_ok(nxt);
+      if (dma_nxt) issue(nxt);
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const bool real = (MODE != 0) || (q * H + j < K);
+      v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pads sort after every real key
+    }
+    bool own = false;
+    const float agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
+    if (own && i < cur.n) {
+      if (cur.out) stg(cur.out + i, agg);
+      if (cur.w) stg(cur.w + i, apply_lr(wv, lr, agg));
+    }
+    cur = nxt;
+    dma_cur = dma_nxt;
+  }
+}
+
+struct LdsArgs {
+  const float* const* peers;
+  const Seg* segs;
+  int nseg;
+  int64_t tiles;  // SEGS: total tiles (tile_begin prefix sums use TW)
+  int K, trim_b;
+  int64_t n;
+  float* w;
+  float* out;
+  float lr;
+  hipStream_t stream;
+};
+
+template <int L, int H, int RULE, int MODE, bool SEGS>
+static void launch_lds_kernel(const LdsArgs& a) {
+  using Lay = LdsLayout<L, H>;
+  auto kern = robust_lds_kernel<L, H, RULE, MODE, SEGS>;
+  static int resident = 0;  // persistent grid: every resident block slot once
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 64 * L, 0);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  const int64_t ntiles = SEGS ? a.tiles : ceil_div(a.n, Lay::TB);
+  const int64_t grid = ntiles < resident ? ntiles : resident;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(64 * L), 0, a.stream, a.peers, a.segs, a.nseg,
+                     ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
+}
+
+template <int L, int H, int RULE, int MODE>
+static void launch_lds_mode(const LdsArgs& a) {
+  if (a.segs) launch_lds_kernel<L, H, RULE, MODE, true>(a);
+  else launch_lds_kernel<L, H, RULE, MODE, false>(a);
+}
+
+template <int L, int H, int RULE>
+static void launch_lds(const LdsArgs& a) {
+  constexpr int KP = L * H;
+  if constexpr (RULE == P2P_RULE_MEDIAN) {
+    if (a.K == KP) return launch_lds_mode<L, H, RULE, 1>(a);
+  } else {
+    if (a.K == KP && a.trim_b == (KP * 2) / 10) return launch_lds_mode<L, H, RULE, 2>(a);
+  }
+  launch_lds_mode<L, H, RULE, 0>(a);
+}
+
+}  // namespace p2p
+
+using namespace p2p;
+
+// Layout for K (p2p_robust_lds_tile and the launch must agree): K in 129..256
+// -> 4 lanes x 64 keys; K in 65..128 -> 4 lanes x 32 keys, or 2 lanes x 64
+// keys when variant == 1 (tuning knob, see robust.hip).
+extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t k, int32_t variant) {
+  return 64;  // every layout: 64-coordinate block tiles
+}
+
+extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, const p2p_segment_t* segs,
+                                                   int32_t nseg, int64_t tiles, int32_t k, int32_t rule,
+                                                   int32_t trim_b, int64_t n, float* w, float* out, float lr,
+                                                   int32_t variant, p2p_stream_t stream) {
+  LdsArgs a{peers, segs, nseg, tiles, k, trim_b, n, w, out, lr, static_cast<hipStream_t>(stream)};
+  const bool med = rule == P2P_RULE_MEDIAN;
+  if (k > 128) {
+    if (med) launch_lds<4, 64, P2P_RULE_MEDIAN>(a); else launch_lds<4, 64, P2P_RULE_TRIMMED>(a);
+  } else if (variant == 1) {
+    if (med) launch_lds<2, 64, P2P_RULE_MEDIAN>(a); else launch_lds<2, 64, P2P_RULE_TRIMMED>(a);
+  } else {
+    if (med) launch_lds<4, 32, P2P_RULE_MEDIAN>(a); else launch_lds<4, 32, P2P_RULE_TRIMMED>(a);
+  }
+}

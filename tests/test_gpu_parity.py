@@ -206,6 +206,79 @@ def test_robust_vs_oracle(cuda, rule, k):
     assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k}")
 
 
+@pytest.fixture(params=["auto", "lds", "lds2", "group"])
+def robust_layout(request):
+    ops.set_robust_layout(request.param)
+    yield request.param
+    ops.set_robust_layout("auto")
+
+
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+@pytest.mark.parametrize("k", [65, 96, 128, 129, 160, 256])
+def test_robust_layouts_many_tiles(cuda, robust_layout, rule, k):
+    """Every K in 65..256 layout over many tiles per wave (persistent loop with
+    the next tile's LDS-DMA in flight) and a ragged tail tile."""
+    peers, w, b, w_ref, out_ref = _many_tiles_case(rule, k)
+    n = w.size
+    wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate([to_dev(p, cuda) for p in peers], rule, w=wt, out=out, trim_b=b)
+    assert_bits_equal(host(out), out_ref, nan_equal=(rule != "median"), what=f"{robust_layout} {rule} K={k}")
+    assert_bits_equal(host(wt), w_ref, what=f"{robust_layout} {rule} apply K={k}")
+
+
+_MANY = {}
+
+
+def _many_tiles_case(rule, k):
+    if (rule, k) not in _MANY:  # the oracle runs once per case, not per layout
+        n = 200_003
+        peers = [oracle.synth(n, 5 * k, p, 1e-2) for p in range(k)]
+        for p in range(0, k, 7):  # ties and special values in a stripe
+            peers[p][1000:1100] = peers[0][1000:1100]
+            peers[p][2000:2003] = np.array([np.inf, -0.0, np.nan], dtype=np.float32)
+        w = oracle.synth(n, 5, 0xFFFFF, 5e-2)
+        b = ops.trim_count(k) if rule == "trimmed" else 0
+        w_ref, out_ref = oracle.robust(peers, ops.rule_id(rule), b, w=w)
+        _MANY[(rule, k)] = (peers, w, b, w_ref, out_ref)
+    return _MANY[(rule, k)]
+
+
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+@pytest.mark.parametrize("k", [100, 256])
+def test_robust_unaligned_views(cuda, robust_layout, rule, k):
+    """Peer views at odd float offsets cannot be LDS-DMA'd (16-B pieces): the
+    register-staged fill must give the same bits."""
+    n = 50_001
+    peers = [oracle.synth(n + 3, 9 * k, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, 9, 0xFFFFF, 5e-2)
+    r = ops.rule_id(rule)
+    b = ops.trim_count(k) if rule == "trimmed" else 0
+    w_ref, out_ref = oracle.robust([p[1 + (i % 3):1 + (i % 3) + n] for i, p in enumerate(peers)], r, b, w=w)
+    dev = [to_dev(p, cuda)[1 + (i % 3):1 + (i % 3) + n] for i, p in enumerate(peers)]
+    wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate(dev, rule, w=wt, out=out, trim_b=b)
+    assert_bits_equal(host(out), out_ref, nan_equal=(rule != "median"), what=f"unaligned {rule} K={k}")
+    assert_bits_equal(host(wt), w_ref, what=f"unaligned {rule} apply K={k}")
+
+
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+@pytest.mark.parametrize("k", [72, 256])
+def test_robust_segments_layouts(cuda, robust_layout, rule, k):
+    """One launch over a state_dict of ragged tensors (segment table)."""
+    sizes = [1, 15, 16, 17, 4099, 33_333, 100_000]
+    n = sum(sizes)
+    peers = [oracle.synth(n, 7 * k, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, 7, 0xFFFFF, 5e-2)
+    b = ops.trim_count(k)
+    w_ref, _ = oracle.robust(peers, ops.rule_id(rule), b if rule == "trimmed" else 0, w=w)
+    offs = np.cumsum([0] + sizes)
+    ws = [to_dev(w[offs[i]:offs[i + 1]], cuda) for i in range(len(sizes))]
+    pl = [[to_dev(p[offs[i]:offs[i + 1]], cuda) for i in range(len(sizes))] for p in peers]
+    ops.aggregate_segments_(ws, pl, rule)
+    got = np.concatenate([host(t) for t in ws])
+    assert_bits_equal(got, w_ref, what=f"segments {robust_layout} {rule} K={k}")
+
+
 @pytest.mark.parametrize("k,b", [(5, 0), (5, 2), (10, 3), (128, 0), (128, 63), (200, 10), (256, 51), (256, 100)])
 def test_trimmed_explicit_b(cuda, k, b):
     n = 1000
