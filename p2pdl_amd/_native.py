@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libp2pdl_hip.so")
+# P2P_LIB selects a diagnostic build (csrc/Makefile `diag`); default: the product library
+LIB_PATH = os.environ.get("P2P_LIB") or os.path.join(_HERE, "libp2pdl_hip.so")
 ABI_VERSION = 1
 
 P2P_RULE_FEDAVG, P2P_RULE_MEDIAN, P2P_RULE_TRIMMED = 0, 1, 2

@@ -40,15 +40,23 @@
 
 #define P2P_LDS __attribute__((address_space(3)))
 
+// Diagnostic builds only (make diag): 1 = no DMA (sort stale LDS: compute
+// time), 2 = no sort (DMA + barriers + stores: staging time).  Wrong results.
+#ifndef P2P_LDS_DIAG
+#define P2P_LDS_DIAG 0
+#endif
+
 namespace p2p {
 
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
   return max(min(a, b), min(max(a, b), c));  // -> v_med3_u32
 }
 
+// DPP move with bound_ctrl: every lane is written, so no "old" operand has to
+// be materialised (update_dpp(0, ...) cost a v_mov_b32 per exchange).
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t x) {
-  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, 0xF, 0xF, false));
+  return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), CTRL, 0xF, 0xF, true));
 }
 // value of lane (lane ^ M) inside the quad
 template <int M>
@@ -72,7 +80,8 @@ struct LdsLayout {
   static constexpr int PAD = L > 1 ? 128 / L : 0;
   static constexpr int SB = H * RB + PAD;      // bytes per slice
   static constexpr int WOFF = L * SB;          // w row
-  static constexpr int BYTES = WOFF + RB;
+  static constexpr int IMG = (WOFF + RB + 15) / 16 * 16;  // one tile image
+  static constexpr int BYTES = 2 * IMG;                   // double-buffered
   static constexpr int CPS = H * RB / 1024;    // 1 KiB DMA pieces per slice (4 rows each)
   static constexpr int NCHW = CPS * L / W;     // DMA pieces per wave per tile
   static_assert((H * RB) % 1024 == 0 && NCHW * W == CPS * L, "slice must be whole 1 KiB DMA pieces");
@@ -227,8 +236,21 @@ __device__ __attribute__((noinline)) void fill_direct(uint8_t P2P_LDS* lds, cons
   if (w && q == 0) ((float P2P_LDS*)(lds + Lay::WOFF))[c] = ldg(w + ic);
 }
 
-__device__ __forceinline__ void block_sync_vm() {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (immediate operand).
+template <int N = 0>
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  if constexpr (N > 24) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (n == N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    else wait_vmcnt<N + 1>(n);
+  }
+}
+
+// Block barrier once this wave's vector-memory ops older than the `younger`
+// most recent ones have completed (the DMA of the tile about to be read).
+__device__ __forceinline__ void block_sync_vm(int younger) {
+  wait_vmcnt(younger);
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
@@ -238,24 +260,33 @@ __device__ __forceinline__ void block_sync_lds() {
   asm volatile("" ::: "memory");
 }
 
+// Block = L sorter waves + L loader waves.  Loaders only issue the LDS-DMA
+// (a global_load_lds costs its wave ~100 cycles of issue; the sorters' VALU
+// stream never pays it); sorters read the image, sort, store.  The block
+// walks tiles t, t+grid, ... with two images: loaders keep the DMA of the
+// next tile in flight while the sorters work on the current one.  Per tile:
+//   loaders: wait own pieces of tile t | barrier A | barrier B | DMA(t+2 grid)
+//   sorters: (fill if not DMA-able)   | barrier A | read      | barrier B | sort, store
 template <int L, int H, int RULE, int MODE, bool SEGS>
-__global__ __launch_bounds__(64 * L) void robust_lds_kernel(const float* const* __restrict__ peers,
-                                                            const Seg* __restrict__ segs, int nseg,
-                                                            int64_t ntiles, int K, int trim_b, int64_t n,
-                                                            float* w, float* out, float lr) {
+__global__ __launch_bounds__(128 * L) void robust_lds_kernel(const float* const* __restrict__ peers,
+                                                             const Seg* __restrict__ segs, int nseg,
+                                                             int64_t ntiles, int K, int trim_b, int64_t n,
+                                                             float* w, float* out, float lr) {
   using Lay = LdsLayout<L, H>;
   __shared__ __attribute__((aligned(16))) uint8_t lds_raw[Lay::BYTES];
   uint8_t P2P_LDS* lds = (uint8_t P2P_LDS*)lds_raw;
   const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
-  const int q = lane % L, c = wi * Lay::TW + lane / L;  // c: coordinate inside the block tile
+  const bool loader = wi >= L;  // wave-uniform role
+  const int li = wi - L;        // loader index
+  const int q = lane % L, c = wi * Lay::TW + lane / L;  // sorters: coordinate inside the block tile
 
   const int64_t nb = gridDim.x;
   int64_t t = blockIdx.x;
   if ((nb & 7) == 0) t = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);  // XCD-contiguous tiles
   if (t >= ntiles) return;
 
-  // per-lane row pointers of this wave's DMA pieces for the current source
+  // loaders: per-lane row pointers of their DMA pieces for the bound source
   const float* rp[Lay::NCHW];
   int64_t cur_seg = -1;
   bool aligned = false;
@@ -263,64 +294,106 @@ __global__ __launch_bounds__(64 * L) void robust_lds_kernel(const float* const* 
     if (s.seg == cur_seg) return;
     cur_seg = s.seg;
     aligned = all_aligned16(s.peers, K, s.w, nullptr);
+    if (loader) {
 #pragma unroll
-    for (int m = 0; m < Lay::NCHW; ++m) {
-      const int ch = wi * Lay::NCHW + m;
-      const int row = (ch / Lay::CPS) * H + (ch % Lay::CPS) * 4 + lane / 16;
-      rp[m] = table_at(s.peers, row < K ? row : K - 1);
+      for (int m = 0; m < Lay::NCHW; ++m) {
+        const int ch = li * Lay::NCHW + m;
+        const int row = (ch / Lay::CPS) * H + (ch % Lay::CPS) * 4 + lane / 16;
+        rp[m] = table_at(s.peers, row < K ? row : K - 1);
+      }
     }
   };
   auto dma_ok = [&](const TileSrc& s) { return aligned && s.c0 + Lay::TB <= s.n; };
-  auto issue = [&](const TileSrc& s) {
+  auto real_piece = [&](int m) {  // pieces made only of pad rows are skipped (MODE 0)
+    const int ch = li * Lay::NCHW + m;
+    return MODE != 0 || (ch / Lay::CPS) * H + (ch % Lay::CPS) * 4 < K;
+  };
+  auto npieces = [&](const TileSrc& s) {
+    int np = 0;
+#pragma unroll
+    for (int m = 0; m < Lay::NCHW; ++m) np += real_piece(m) ? 1 : 0;
+    return np + ((s.w && li == 0) ? 1 : 0);
+  };
+  auto issue = [&](const TileSrc& s, int img_off) {
+    if constexpr (P2P_LDS_DIAG == 1) return;
+    uint8_t P2P_LDS* im = lds + img_off;
     const int64_t off = s.c0 + 4 * (lane % 16);
 #pragma unroll
     for (int m = 0; m < Lay::NCHW; ++m) {
-      const int ch = wi * Lay::NCHW + m;
-      const int row0 = (ch / Lay::CPS) * H + (ch % Lay::CPS) * 4;
-      if (MODE != 0 || row0 < K)  // wave-uniform: pieces made only of pad rows are skipped
-        glds16(rp[m] + off, lds + (ch / Lay::CPS) * Lay::SB + (ch % Lay::CPS) * 1024);
+      const int ch = li * Lay::NCHW + m;
+      if (real_piece(m)) glds16(rp[m] + off, im + (ch / Lay::CPS) * Lay::SB + (ch % Lay::CPS) * 1024);
     }
-    if (s.w && wi == 0 && lane < 16) glds16(s.w + s.c0 + 4 * lane, lds + Lay::WOFF);
+    if (s.w && li == 0 && lane < 16) glds16(s.w + s.c0 + 4 * lane, im + Lay::WOFF);
   };
 
   TileSrc cur = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t);
   bind(cur);
   bool dma_cur = dma_ok(cur);
-  if (dma_cur) issue(cur);
+  if (loader && dma_cur) issue(cur, 0);
+  TileSrc nx1 = cur;
+  bool dma_nx1 = false;
+  if (t + nb < ntiles) {
+    nx1 = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t + nb);
+    bind(nx1);
+    dma_nx1 = dma_ok(nx1);
+    if (loader && dma_nx1) issue(nx1, Lay::IMG);
+  }
+  int img = 0;
 
   for (; t < ntiles; t += nb) {
+    uint8_t P2P_LDS* im = lds + img;
     const int64_t i = cur.c0 + c;
-    if (!dma_cur) fill_direct<L, H>(lds, cur.peers, cur.w, cur.n, i, K, q, c);
-    block_sync_vm();  // every wave's DMA pieces have landed
     uint32_t v[H];
-    {
-      const uint32_t P2P_LDS* sl = (const uint32_t P2P_LDS*)(lds + q * Lay::SB) + c;
+    float wv = 0.f;
+    if (loader) {
+      block_sync_vm(dma_nx1 ? npieces(nx1) : 0);  // A: this loader's pieces of tile t landed
+      __builtin_amdgcn_s_barrier();               // B: sorters have read the image
+      asm volatile("" ::: "memory");
+    } else {
+      if (!dma_cur) fill_direct<L, H>(im, cur.peers, cur.w, cur.n, i, K, q, c);
+      __builtin_amdgcn_s_barrier();  // A: every piece of tile t is in the image
+      asm volatile("" ::: "memory");
+      const uint32_t P2P_LDS* sl = (const uint32_t P2P_LDS*)(im + q * Lay::SB) + c;
 #pragma unroll
       for (int j = 0; j < H; ++j) v[j] = sl[j * (Lay::RB / 4)];
+      if (cur.w) wv = ((const float P2P_LDS*)(im + Lay::WOFF))[c];
+      block_sync_lds();  // B: image consumed, free for the DMA two tiles ahead
     }
-    const float wv = cur.w ? ((const float P2P_LDS*)(lds + Lay::WOFF))[c] : 0.f;
-    block_sync_lds();  // image consumed: free for the next tile's DMA
-    // prefetch the next tile of this block while this one is sorted
-    const TileSrc nxt = (t + nb < ntiles) ? locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t + nb) : cur;
-    bool dma_nxt = false;
-    if (t + nb < ntiles) {
-      bind(nxt);
-      dma_nxt = dma_ok(nxt);
-      if (dma_nxt) issue(nxt);
+    TileSrc nx2 = nx1;
+    bool dma_nx2 = false;
+    if (t + 2 * nb < ntiles) {
+      nx2 = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t + 2 * nb);
+      bind(nx2);
+      dma_nx2 = dma_ok(nx2);
+      if (loader && dma_nx2) issue(nx2, img);
     }
+    if (!loader) {
 #pragma unroll
-    for (int j = 0; j < H; ++j) {
-      const bool real = (MODE != 0) || (q * H + j < K);
-      v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pads sort after every real key
+      for (int j = 0; j < H; ++j) {
+        const bool real = (MODE != 0) || (q * H + j < K);
+        v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pads sort after every real key
+      }
+      bool own = false;
+      float agg;
+      if constexpr (P2P_LDS_DIAG == 2) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < H; ++j) x ^= v[j];
+        agg = __uint_as_float(x);
+        own = q == 0;
+      } else {
+        agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
+      }
+      if (own && i < cur.n) {
+        if (cur.out) stg(cur.out + i, agg);
+        if (cur.w) stg(cur.w + i, apply_lr(wv, lr, agg));
+      }
     }
-    bool own = false;
-    const float agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
-    if (own && i < cur.n) {
-      if (cur.out) stg(cur.out + i, agg);
-      if (cur.w) stg(cur.w + i, apply_lr(wv, lr, agg));
-    }
-    cur = nxt;
-    dma_cur = dma_nxt;
+    cur = nx1;
+    dma_cur = dma_nx1;
+    nx1 = nx2;
+    dma_nx1 = dma_nx2;
+    img ^= Lay::IMG;
   }
 }
 
@@ -346,12 +419,12 @@ static void launch_lds_kernel(const LdsArgs& a) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 64 * L, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 128 * L, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int64_t ntiles = SEGS ? a.tiles : ceil_div(a.n, Lay::TB);
   const int64_t grid = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(64 * L), 0, a.stream, a.peers, a.segs, a.nseg,
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(128 * L), 0, a.stream, a.peers, a.segs, a.nseg,
                      ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
 }
 

@@ -7,9 +7,9 @@
 
 namespace p2p {
 
-template <bool ASC>
-__device__ __forceinline__ void ce(uint32_t& a, uint32_t& b) {
-  const uint32_t lo = min(a, b), hi = max(a, b);
+template <bool ASC, typename T>
+__device__ __forceinline__ void ce(T& a, T& b) {
+  const T lo = min(a, b), hi = max(a, b);
   if constexpr (ASC) { a = lo; b = hi; } else { a = hi; b = lo; }
 }
 #define P2P_CE(a, b) ce<ASC>((a), (b))
@@ -20,25 +20,30 @@ __device__ __forceinline__ void ce(uint32_t& a, uint32_t& b) {
 #undef P2P_MIN
 #undef P2P_MAX
 
-template <int KP, bool ASC = true> __device__ __forceinline__ void sort_full(uint32_t (&v)[KP]);
-#define P2P_SORT(KP) \
-  template <> __device__ __forceinline__ void sort_full<KP, true>(uint32_t (&v)[KP]) { net_sort##KP<true>(v); } \
-  template <> __device__ __forceinline__ void sort_full<KP, false>(uint32_t (&v)[KP]) { net_sort##KP<false>(v); }
-P2P_SORT(2) P2P_SORT(4) P2P_SORT(8) P2P_SORT(16) P2P_SORT(32) P2P_SORT(64) P2P_SORT(128)
-#undef P2P_SORT
+template <int KP, bool ASC = true, typename T> __device__ __forceinline__ void sort_full(T (&v)[KP]) {
+  if constexpr (KP == 2) net_sort2<ASC>(v);
+  else if constexpr (KP == 4) net_sort4<ASC>(v);
+  else if constexpr (KP == 8) net_sort8<ASC>(v);
+  else if constexpr (KP == 16) net_sort16<ASC>(v);
+  else if constexpr (KP == 32) net_sort32<ASC>(v);
+  else if constexpr (KP == 64) net_sort64<ASC>(v);
+  else net_sort128<ASC>(v);
+}
 
 // Sorts a bitonic sequence of KP keys ascending (half-cleaners n/2 .. 1).
-template <int KP> __device__ __forceinline__ void bmerge(uint32_t (&v)[KP]);
-template <> __device__ __forceinline__ void bmerge<32>(uint32_t (&v)[32]) { net_bmerge32<true>(v); }
-template <> __device__ __forceinline__ void bmerge<64>(uint32_t (&v)[64]) { net_bmerge64<true>(v); }
+template <int KP, typename T> __device__ __forceinline__ void bmerge(T (&v)[KP]) {
+  if constexpr (KP == 32) net_bmerge32<true>(v);
+  else net_bmerge64<true>(v);
+}
 
 // MODE 0: generic (full sort + runtime rank / trim);
 // MODE 1: pruned median network for K == KP;
 // MODE 2: pruned trimmed network for K == KP, b == floor(0.2 KP).
-template <int KP, int MODE> __device__ __forceinline__ void run_special(uint32_t (&v)[KP]);
-template <> __device__ __forceinline__ void run_special<64, 1>(uint32_t (&v)[64]) { net_median64<true>(v); }
-template <> __device__ __forceinline__ void run_special<128, 1>(uint32_t (&v)[128]) { net_median128<true>(v); }
-template <> __device__ __forceinline__ void run_special<64, 2>(uint32_t (&v)[64]) { net_trim64_b12<true>(v); }
-template <> __device__ __forceinline__ void run_special<128, 2>(uint32_t (&v)[128]) { net_trim128_b25<true>(v); }
+template <int KP, int MODE, typename T> __device__ __forceinline__ void run_special(T (&v)[KP]) {
+  if constexpr (KP == 64 && MODE == 1) net_median64<true>(v);
+  else if constexpr (KP == 128 && MODE == 1) net_median128<true>(v);
+  else if constexpr (KP == 64 && MODE == 2) net_trim64_b12<true>(v);
+  else net_trim128_b25<true>(v);
+}
 
 }  // namespace p2p
