@@ -50,6 +50,8 @@ WORKLOADS = {
     "cfg5": ("fused", 256, 25_000_000, 0x5EED0004),
     # SHA-256 alone over 256 messages of the cfg5 size
     "sha256": ("sha256", 256, 25_000_000, 0x5EED0004),
+    # trainer-side delta + snapshot of cfg3's 1B-param model
+    "delta": ("delta", 1, 1_000_000_000, 0x5EED0006),
 }
 MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
@@ -184,6 +186,68 @@ def run_digest_workload(args, rule, K, n, seed, dev):
     print(json.dumps(line), flush=True)
 
 
+def run_delta_workload(args, n, seed, dev):
+    """Trainer-side local update (reference node/node.py:273-282) of one
+    flat n-parameter model: delta = cur - prev; prev = cur.  One GPU."""
+    import numpy as np
+
+    cur = torch.empty(n, dtype=torch.float32, device=dev)
+    prev = torch.empty_like(cur)
+    delta = torch.empty_like(cur)
+    ops.fill_synthetic_(cur, seed, 1, 1e-1)
+    ops.fill_synthetic_(prev, seed, 2, 1e-1)
+    comp = torch.cuda.current_stream(dev)
+    if not args.no_check:  # one launch, checked against the oracle on a prefix
+        import oracle  # checker only
+
+        m = min(n, 1 << 20)
+        ops.delta_snapshot_(cur, prev, delta)
+        torch.cuda.synchronize()
+        want, _ = oracle.delta_snapshot_np(oracle.synth(m, seed, 1, 1e-1), oracle.synth(m, seed, 2, 1e-1))
+        ok = np.array_equal(delta[:m].cpu().numpy().view(np.uint32), want.view(np.uint32)) and \
+            torch.equal(prev[:m], cur[:m])
+        log(f"spot check vs oracle ({m} coords): {'bit-exact' if ok else 'MISMATCH'}")
+        if not ok:
+            raise SystemExit("bench: delta kernel differs from the oracle")
+    for _ in range(max(args.warmup, 1)):
+        ops.delta_snapshot_(cur, prev, delta)
+    torch.cuda.synchronize()
+    ev = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(comp)
+        ops.delta_snapshot_(cur, prev, delta)
+        e1.record(comp)
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    step_s = (time.perf_counter() - t0) / args.steps
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    alg = 16 * n
+    cpu = None
+    if not args.no_cpu_baseline:
+        import oracle.cpu_baseline as cb  # baseline leg only
+
+        torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+        n_s = 50_000_000
+        gbs, thr, reps, el = cb.time_delta(n_s, args.cpu_seconds)
+        cpu = {"value": round(gbs, 3), "unit": "GB/s", "cores": thr, "kind": "port",
+               "sample": f"{n_s:,} fp32 params, reference ops cur - prev and clone (node/node.py:279,282) "
+                         f"on torch CPU, {reps} reps in {el:.1f}s"}
+    print(json.dumps({
+        "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
+        "value": round(alg / step_s / 1e9, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (device counter PRNG); value = algorithmic bytes (16 B/param) per second",
+        "config": {"workload": f"delta: trainer local update over {n:,} fp32 params (SURVEY §8(f) row 2)",
+                   "coords_per_gpu": n, "parallelism": "single GPU (replicas only)"},
+        "roofline": {"bound": "hbm", "achieved": round(alg / (kern_ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(alg / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg},
+        "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -210,6 +274,10 @@ def main():
         if world > 1:
             raise SystemExit("cfg5/sha256 run as replicas only (one process per GPU)")
         return run_digest_workload(args, rule, K, n, seed, dev)
+    if rule == "delta":
+        if world > 1:
+            raise SystemExit("delta runs as replicas only (one process per GPU)")
+        return run_delta_workload(args, n, seed, dev)
     S = args.chunks if world > 1 else 1
     C = -(-n // S)
     n = C * S  # whole chunks per rank

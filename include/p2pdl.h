@@ -110,6 +110,29 @@ int32_t p2p_set_robust_layout(int32_t layout);
 /* w += lr * agg, multiply and add separately rounded (aggregation.py:36-38). */
 int32_t p2p_apply_f32(float *w, const float *agg, float lr, int64_t n, p2p_stream_t stream);
 
+/* ---- K4: trainer-side local update ---------------
+ * Replaces reference node/node.py:273-282: delta = current - previous
+ * (:278-279), then previous = current (the clone at :282).  first != 0 is
+ * the first round (previous is None, :272-275): delta = current.  One pass,
+ * 16 bytes of HBM traffic per coordinate; fp32 subtraction is IEEE exact. */
+int32_t p2p_delta_snapshot_f32(const float *cur, float *prev, float *delta, int64_t n, int32_t first,
+                               p2p_stream_t stream);
+
+#define P2P_DELTA_TILE 4096 /* elements per tile of the delta segment kernel */
+
+/* One tensor of a state_dict for the delta kernel (device-resident entry). */
+typedef struct p2p_delta_segment_t {
+  const float *cur; /* current parameter (model.state_dict()[key]) */
+  float *prev;      /* previous snapshot, overwritten with cur */
+  float *delta;     /* receives cur - prev */
+  int64_t n;
+  int64_t tile_begin; /* sum of ceil(n_j / P2P_DELTA_TILE) over earlier segments */
+} p2p_delta_segment_t;
+
+/* Whole state_dict in one launch (segs is a DEVICE array). */
+int32_t p2p_delta_snapshot_segments_f32(const p2p_delta_segment_t *segs, int32_t nseg, int64_t total_tiles,
+                                        int32_t first, p2p_stream_t stream);
+
 /* ---- K3: SHA-256 over serialized updates --------------------------------
  * digests[32*i .. 32*i+31] = SHA-256(msgs[i][0 .. lens[i]-1]) (FIPS 180-4),
  * the digest inside ECDSA(SHA256()) of reference utils/crypto.py:54-57 (sign)

@@ -180,3 +180,14 @@ def sha256(data: bytes) -> bytes:
     out = np.zeros(32, dtype=np.uint8)
     lib().oracle_sha256(_ptr(buf), len(data), _ptr(out))
     return out.tobytes()
+
+
+def delta_snapshot_np(cur, prev=None):
+    """Trainer-side local update, reference node/node.py:272-282: the first
+    round (prev None) sends the current state (:275), later rounds
+    current - previous (:279, fp32 IEEE subtraction); the new previous is a
+    copy of current (:282).  Returns (delta, new_prev)."""
+    cur = np.ascontiguousarray(cur, dtype=np.float32)
+    if prev is None:
+        return cur.copy(), cur.copy()
+    return (cur - np.asarray(prev, dtype=np.float32)).astype(np.float32), cur.copy()

@@ -61,3 +61,24 @@ def time_median(k: int, n: int, target_s: float = 12.0, seed: int = 0x5EED0003):
         if el >= target_s:
             break
     return k * n * 4 * reps / el / 1e9, torch.get_num_threads(), reps, el
+
+
+def reference_ops_delta(cur: torch.Tensor, prev: torch.Tensor):
+    """Reference node/node.py:279,282 on one flat buffer: sub, then clone."""
+    return cur - prev, cur.clone()
+
+
+def time_delta(n: int, target_s: float = 12.0, seed: int = 0x5EED0006):
+    """GB/s of algorithmic traffic (16 B per coordinate: read cur, read prev,
+    write delta, write the new snapshot) of the reference's torch CPU ops."""
+    cur = torch.from_numpy(oracle.synth(n, seed, 1, 1e-1))
+    prev = torch.from_numpy(oracle.synth(n, seed, 2, 1e-1))
+    reference_ops_delta(cur, prev)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        reference_ops_delta(cur, prev)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= target_s:
+            break
+    return 16 * n * reps / el / 1e9, torch.get_num_threads(), reps, el

@@ -1,0 +1,120 @@
+// K4 -- trainer-side local update for gfx950.
+//
+// Replaces reference node/node.py:273-282 (Node.send_model_to_testers):
+//   local_update[key] = current[key] - previous[key]      (:278-279)
+//   previous = {key: current[key].clone()}                 (:282)
+// and, on the first round (previous is None, :272-275), local_update = current.
+// The reference runs one sub kernel and one clone per key (20 B of traffic
+// per coordinate over 2L launches); here ONE pass per state_dict reads
+// current and previous and writes delta and the new previous: 16 B per
+// coordinate, HBM-bound (0.0625 flop/B).  fp32 subtraction is IEEE, so the
+// result is bit-exact with torch's CPU/GPU `-`.
+//
+// Layout as K1 (fedavg.hip): a 256-lane block owns a 4096-float tile, lane l
+// the float4s l, l+256, l+512, l+768 -> every wave instruction moves one
+// contiguous 1 KiB.  Misaligned views and ragged tails go element-wise.
+#include "p2p_common.h"
+
+namespace p2p {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int kDNV = 4;
+constexpr int kDTile = kBlock * 4 * kDNV;  // 4096 floats
+
+__device__ __forceinline__ f4 ld4_nt(const float* p) { return ldg_nt(reinterpret_cast<const f4*>(p)); }
+__device__ __forceinline__ void st4_nt(float* p, f4 v) {
+  __builtin_nontemporal_store(v, (P2P_GLOBAL f4*)(p));
+}
+
+__device__ __forceinline__ void delta_tile(const float* cur, float* prev, float* delta, int64_t n,
+                                           int64_t tile0, bool first) {
+  const int64_t base = tile0 + 4 * static_cast<int64_t>(threadIdx.x);
+  const bool aligned =
+      ((reinterpret_cast<uintptr_t>(cur) | reinterpret_cast<uintptr_t>(prev) | reinterpret_cast<uintptr_t>(delta)) &
+       15) == 0;
+  if (aligned && tile0 + kDTile <= n) {
+    f4 c[kDNV], p[kDNV];
+#pragma unroll
+    for (int v = 0; v < kDNV; ++v) c[v] = ld4_nt(cur + base + kBlock * 4 * v);
+    if (!first) {
+#pragma unroll
+      for (int v = 0; v < kDNV; ++v) p[v] = ld4_nt(prev + base + kBlock * 4 * v);
+    }
+#pragma unroll
+    for (int v = 0; v < kDNV; ++v) {
+      const int64_t o = base + kBlock * 4 * v;
+      st4_nt(delta + o, first ? c[v] : c[v] - p[v]);  // (:279) or the first-round copy (:275)
+      st4_nt(prev + o, c[v]);                          // clone (:282)
+    }
+    return;
+  }
+#pragma unroll 1
+  for (int v = 0; v < kDNV; ++v)
+#pragma unroll 1
+    for (int e = 0; e < 4; ++e) {
+      const int64_t i = base + kBlock * 4 * v + e;
+      if (i >= n) continue;
+      const float x = ldg(cur + i);
+      stg(delta + i, first ? x : x - ldg(prev + i));
+      stg(prev + i, x);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void delta_flat_kernel(const float* cur, float* prev, float* delta,
+                                                            int64_t n, int first) {
+  delta_tile(cur, prev, delta, n, static_cast<int64_t>(blockIdx.x) * kDTile, first != 0);
+}
+
+// Whole state_dict: one tile per block, segment by binary search on tile_begin.
+__global__ __launch_bounds__(kBlock) void delta_segments_kernel(const p2p_delta_segment_t* __restrict__ segs,
+                                                                int nseg, int first) {
+  const int64_t t = blockIdx.x;
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    const int64_t tb = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&segs[mid].tile_begin))));
+    if (tb <= t) lo = mid; else hi = mid - 1;
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+  }
+  const p2p_delta_segment_t* sp = segs + lo;
+  const float* cur = reinterpret_cast<const float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->cur))));
+  float* prev = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->prev))));
+  float* delta = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->delta))));
+  const int64_t n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
+  const int64_t tb = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->tile_begin))));
+  delta_tile(cur, prev, delta, n, (t - tb) * kDTile, first != 0);
+}
+
+}  // namespace p2p
+
+using namespace p2p;
+
+static int32_t delta_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? P2P_OK : static_cast<int32_t>(e);
+}
+
+extern "C" int32_t p2p_delta_snapshot_f32(const float* cur, float* prev, float* delta, int64_t n, int32_t first,
+                                          p2p_stream_t stream) {
+  if (!cur || !prev || !delta || n < 0) return P2P_ERR_INVALID;
+  if ((reinterpret_cast<uintptr_t>(cur) | reinterpret_cast<uintptr_t>(prev) | reinterpret_cast<uintptr_t>(delta)) &
+      3)
+    return P2P_ERR_ALIGN;
+  if (n == 0) return P2P_OK;
+  const int64_t tiles = ceil_div(n, kDTile);
+  if (tiles > 0x7FFFFFFFll) return P2P_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(delta_flat_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), cur, prev, delta, n, first);
+  return delta_status();
+}
+
+extern "C" int32_t p2p_delta_snapshot_segments_f32(const p2p_delta_segment_t* segs, int32_t nseg,
+                                                   int64_t total_tiles, int32_t first, p2p_stream_t stream) {
+  if (!segs || nseg < 1 || total_tiles < 0) return P2P_ERR_INVALID;
+  if (total_tiles > 0x7FFFFFFFll) return P2P_ERR_UNSUPPORTED;
+  if (total_tiles == 0) return P2P_OK;
+  hipLaunchKernelGGL(delta_segments_kernel, dim3(static_cast<unsigned>(total_tiles)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), segs, nseg, first);
+  return delta_status();
+}

@@ -196,6 +196,53 @@ def aggregate_segments_(ws: Sequence[torch.Tensor], peer_lists: Sequence[Sequenc
     buf.record_stream(torch.cuda.current_stream(dev))
 
 
+# ------------------------------------------------------------------ K4
+DELTA_TILE = 4096  # == P2P_DELTA_TILE
+_DSEG_DTYPE = np.dtype([("cur", "<u8"), ("prev", "<u8"), ("delta", "<u8"), ("n", "<i8"),
+                        ("tile_begin", "<i8")])  # == p2p_delta_segment_t (40 B)
+
+
+def delta_snapshot_(cur: torch.Tensor, prev: torch.Tensor, delta: torch.Tensor, first: bool = False) -> None:
+    """delta = cur - prev; prev = cur (first: delta = cur), one pass
+    (reference node/node.py:273-282 for one flat buffer)."""
+    N.require_device(cur)
+    for name, t in (("cur", cur), ("prev", prev), ("delta", delta)):
+        _check_f32(t, name, cur.device)
+        if t.numel() != cur.numel():
+            raise ValueError(f"{name} has {t.numel()} elements, expected {cur.numel()}")
+    with torch.cuda.device(cur.device):
+        N.check(N.lib().p2p_delta_snapshot_f32(cur.data_ptr(), prev.data_ptr(), delta.data_ptr(), cur.numel(),
+                                               int(first), N.stream_handle()), "p2p_delta_snapshot_f32")
+
+
+def delta_snapshot_segments_(curs: Sequence[torch.Tensor], prevs: Sequence[torch.Tensor],
+                             deltas: Sequence[torch.Tensor], first: bool = False) -> None:
+    """Whole state_dict in ONE launch: deltas[l] = curs[l] - prevs[l]; prevs[l] = curs[l]."""
+    L = len(curs)
+    if L == 0:
+        return
+    if not (len(prevs) == len(deltas) == L):
+        raise ValueError("curs, prevs and deltas must have the same length")
+    dev = curs[0].device
+    N.require_device(curs[0])
+    segs = np.zeros(L, dtype=_DSEG_DTYPE)
+    tiles = 0
+    for l, (c, p, d) in enumerate(zip(curs, prevs, deltas)):
+        for name, t in (("cur", c), ("prev", p), ("delta", d)):
+            _check_f32(t, f"{name}[{l}]", dev)
+            if t.numel() != c.numel():
+                raise ValueError(f"{name}[{l}] has {t.numel()} elements, expected {c.numel()}")
+        segs[l] = (c.data_ptr(), p.data_ptr(), d.data_ptr(), c.numel(), tiles)
+        tiles += -(-c.numel() // DELTA_TILE)
+    if tiles == 0:
+        return
+    buf = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
+    with torch.cuda.device(dev):
+        N.check(N.lib().p2p_delta_snapshot_segments_f32(buf.data_ptr(), L, tiles, int(first), N.stream_handle()),
+                "p2p_delta_snapshot_segments_f32")
+    buf.record_stream(torch.cuda.current_stream(dev))
+
+
 # ------------------------------------------------------------------ K3
 def sha256_batch_device(msgs: torch.Tensor, offsets: Sequence[int], lengths: Sequence[int]) -> torch.Tensor:
     """Digest K messages that live in one device uint8 buffer.

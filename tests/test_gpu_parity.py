@@ -318,6 +318,76 @@ def test_dropin_robust_rules(cuda, rule, k, monkeypatch):
     assert_bits_equal(out, w_ref, what=f"dropin {rule}")
 
 
+# ------------------------------------------------------------------ K4 trainer delta
+@pytest.mark.parametrize("n", [1, 3, 4096, 4097, 100_003])
+@pytest.mark.parametrize("first", [False, True])
+def test_delta_snapshot_flat(cuda, n, first):
+    cur = oracle.synth(n, 21, 1, 1e-1)
+    prev = oracle.synth(n, 21, 2, 1e-1)
+    if n > 10:
+        cur[:4] = np.array([np.inf, -0.0, 0.0, 1e-40], dtype=np.float32)
+        prev[:4] = np.array([1.0, 0.0, -0.0, 1e-40], dtype=np.float32)
+    d_ref, p_ref = oracle.delta_snapshot_np(cur, None if first else prev)
+    c, p = to_dev(cur, cuda), to_dev(prev, cuda)
+    d = torch.empty_like(c)
+    ops.delta_snapshot_(c, p, d, first=first)
+    assert_bits_equal(host(d), d_ref, what="delta")
+    assert_bits_equal(host(p), p_ref, what="snapshot")
+    if not first:  # and the reference op itself (torch `-`, node/node.py:279)
+        assert_bits_equal(host(d), (torch.from_numpy(cur) - torch.from_numpy(prev)).numpy(), what="torch sub")
+
+
+def test_delta_snapshot_unaligned_and_segments(cuda):
+    sizes = [1, 5, 4095, 4096, 4099, 70_001]
+    n = sum(sizes)
+    cur = oracle.synth(n + 1, 22, 1, 1e-1)
+    prev = oracle.synth(n + 1, 22, 2, 1e-1)
+    cd, pd = to_dev(cur, cuda), to_dev(prev, cuda)
+    offs = np.cumsum([0] + sizes)
+    curs = [cd[1 + offs[i]:1 + offs[i + 1]] for i in range(len(sizes))]  # odd offsets: element path
+    prevs = [pd[1 + offs[i]:1 + offs[i + 1]] for i in range(len(sizes))]
+    deltas = [torch.empty(s, dtype=torch.float32, device=cuda) for s in sizes]
+    ops.delta_snapshot_segments_(curs, prevs, deltas)
+    d_ref, _ = oracle.delta_snapshot_np(cur[1:n + 1], prev[1:n + 1])
+    assert_bits_equal(np.concatenate([host(x) for x in deltas]), d_ref, what="segments delta")
+    assert_bits_equal(host(pd)[1:n + 1], cur[1:n + 1], what="segments snapshot")
+
+
+def test_compute_local_update_dropin(cuda):
+    """Three rounds of reference node/node.py:267-282 vs the drop-in, on a
+    model with an int64 buffer (BatchNorm) next to the fp32 parameters."""
+    from p2pdl_amd.node.local_update import compute_local_update
+
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(33, 64), torch.nn.BatchNorm1d(64), torch.nn.Linear(64, 10))
+    ref_model = torch.nn.Sequential(torch.nn.Linear(33, 64), torch.nn.BatchNorm1d(64), torch.nn.Linear(64, 10))
+    ref_model.load_state_dict(net.state_dict())
+    node = types.SimpleNamespace(model=net.to(cuda), previous_model_state=None)
+    ref_prev = None
+    for rnd in range(3):
+        with torch.no_grad():  # a "training step": perturb every parameter, bump the buffer
+            for (_, p), (_, q) in zip(node.model.named_parameters(), ref_model.named_parameters()):
+                noise = torch.randn(p.shape) * 1e-2
+                p.add_(noise.to(cuda))
+                q.add_(noise)
+            node.model[1].num_batches_tracked += 1
+            ref_model[1].num_batches_tracked += 1
+        got = compute_local_update(node)
+        cur = ref_model.state_dict()  # reference :267-282 on CPU
+        want = {k: cur[k] for k in cur} if ref_prev is None else {k: cur[k] - ref_prev[k] for k in cur}
+        ref_prev = {k: v.clone() for k, v in cur.items()}
+        assert list(got) == list(want)
+        for k in want:
+            g = got[k].detach().cpu()
+            assert g.dtype == want[k].dtype and g.shape == want[k].shape, k
+            if g.is_floating_point():
+                assert_bits_equal(g.numpy(), want[k].numpy(), what=f"round {rnd} {k}")
+            else:
+                assert torch.equal(g, want[k]), k
+        for k in ref_prev:
+            assert torch.equal(node.previous_model_state[k].cpu(), ref_prev[k]), k
+
+
 # ------------------------------------------------------------------ SHA-256
 KATS = [
     (b"", "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"),

@@ -87,3 +87,16 @@ def test_sorting_networks_0_1_principle():
     import gen_networks
 
     gen_networks.check()
+
+
+def test_delta_snapshot_oracle_matches_torch_reference_ops():
+    """oracle.delta_snapshot_np == the reference's torch ops (node/node.py:275,279,282)."""
+    import torch
+
+    cur = oracle.synth(10_001, 3, 1, 1e-1)
+    prev = oracle.synth(10_001, 3, 2, 1e-1)
+    d, p = oracle.delta_snapshot_np(cur, prev)
+    assert np.array_equal(d.view(np.uint32), (torch.from_numpy(cur) - torch.from_numpy(prev)).numpy().view(np.uint32))
+    assert np.array_equal(p, cur)
+    d0, p0 = oracle.delta_snapshot_np(cur, None)
+    assert np.array_equal(d0, cur) and np.array_equal(p0, cur) and d0 is not cur
