@@ -5,10 +5,13 @@
 // bytes of pickle.dumps(local_update) (node/node.py:285).  Each message is a
 // serial Merkle-Damgard chain, so the only parallelism is across messages:
 // one lane owns one message and runs its compression chain in VGPRs.  The
-// round function uses gfx950's 3-input ops (v_xor3_b32 for the Sigma/sigma
-// XORs, v_add3_u32 for the T1 sums, v_alignbit_b32 rotates, v_bfi_b32 for
-// Ch / Maj) -- about 1.5k VALU instructions per 64-B block.  This kernel is
-// bounded by per-lane serial INT-ALU issue, not by HBM; DESIGN.md prices it.
+// round function uses gfx950's 3-input ops (v_bitop3_b32 for the Sigma XORs
+// and Ch / Maj, v_add3_u32 for the sums, v_alignbit_b32 rotates).  With 256
+// messages only 4 waves carry chains, and a lone wave issues about one
+// instruction per ~5.5 cycles (profiles/r01/probes), so a block costs
+// (instructions on the chain) x 5.5 cycles: the schedule expansion is moved
+// to a second wave (sha256_pair_kernel).  Bounded by per-wave serial issue,
+// not by HBM; DESIGN.md prices it.
 #include "p2p_common.h"
 
 namespace p2p {
@@ -27,30 +30,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int r) { return __builtin_rotateright32(x, r); }
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
-
-__device__ __forceinline__ void compress(uint32_t (&h)[8], uint32_t (&W)[16]) {
-  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#pragma unroll
-  for (int t = 0; t < 64; ++t) {
-    uint32_t wt;
-    if (t < 16) {
-      wt = W[t];
-    } else {
-      const uint32_t w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
-      const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
-      wt = W[t & 15] + s0 + W[(t - 7) & 15] + s1;
-      W[t & 15] = wt;
-    }
-    const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
-    const uint32_t ch = (e & f) ^ (~e & g);
-    const uint32_t T1 = hh + S1 + ch + kK256[t] + wt;
-    const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
-    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-    const uint32_t T2 = S0 + mj;
-    hh = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + T2;
-  }
-  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+// a ^ b ^ c in one v_bitop3_b32 (truth table 0x96); hipcc emits two v_xor_b32
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
 // Byte j (0..63) of the padded tail region of a message of `len` bytes whose
@@ -64,25 +46,46 @@ __device__ __forceinline__ uint32_t tail_byte(const uint8_t* tail, uint32_t rem,
   return 0u;
 }
 
-__global__ __launch_bounds__(64) void sha256_batch_kernel(const uint8_t* const* __restrict__ msgs,
-                                                          const uint64_t* __restrict__ lens, int k,
-                                                          uint8_t* __restrict__ digests) {
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= k) return;
-  const uint8_t* m = ldg(msgs + i);
-  const uint64_t len = ldg(lens + i);
-  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
-                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+// Message schedule of one block, K folded in: kw[t] = K[t] + W[t].
+__device__ __forceinline__ void schedule_kw(uint32_t (&W)[64]) {
+#pragma unroll
+  for (int t = 16; t < 64; ++t) {
+    const uint32_t w15 = W[t - 15], w2 = W[t - 2];
+    const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+    const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+    W[t] = W[t - 16] + s0 + W[t - 7] + s1;
+  }
+#pragma unroll
+  for (int t = 0; t < 64; ++t) W[t] += kK256[t];
+}
+
+// 64 rounds with the schedule already expanded (kw = K + W).
+__device__ __forceinline__ void rounds_kw(uint32_t (&h)[8], const uint32_t (&kw)[64]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);  // e ? f : g
+    const uint32_t T1 = hh + S1 + ch + kw[t];
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);  // majority
+    hh = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + S0 + mj;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// Words 0..15 of block `blk` of a message (message blocks, then the 1 or 2
+// padding blocks: 0x80, zeros, 64-bit big-endian bit length).
+__device__ __forceinline__ void load_block(uint32_t (&W)[64], const uint8_t* m, uint64_t len, uint64_t blk,
+                                           bool al16) {
   const uint64_t full = len >> 6;
-  const bool al16 = (reinterpret_cast<uintptr_t>(m) & 15) == 0;
-  uint32_t W[16];
-  for (uint64_t blk = 0; blk < full; ++blk) {
+  if (blk < full) {
     const uint8_t* p = m + (blk << 6);
     if (al16) {
       const u32x4* q = reinterpret_cast<const u32x4*>(p);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const u32x4 x = ldg(q + j);
+        const u32x4 x = ldg_nt(q + j);
         W[4 * j] = bswap(x.x); W[4 * j + 1] = bswap(x.y);
         W[4 * j + 2] = bswap(x.z); W[4 * j + 3] = bswap(x.w);
       }
@@ -92,25 +95,90 @@ __global__ __launch_bounds__(64) void sha256_batch_kernel(const uint8_t* const* 
         W[j] = (uint32_t(ldg(p + 4 * j)) << 24) | (uint32_t(ldg(p + 4 * j + 1)) << 16) |
                (uint32_t(ldg(p + 4 * j + 2)) << 8) | uint32_t(ldg(p + 4 * j + 3));
     }
-    compress(h, W);
+    return;
   }
-  // Padding: 0x80, zeros, 64-bit big-endian bit length; 1 or 2 blocks.
   const uint32_t rem = static_cast<uint32_t>(len & 63);
   const uint32_t nblk = (rem + 9u <= 64u) ? 1u : 2u;
   const uint8_t* tail = m + (full << 6);
   const uint64_t bits = len * 8u;
-  for (uint32_t tb = 0; tb < nblk; ++tb) {
+  const uint32_t tb = static_cast<uint32_t>(blk - full);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t o = tb * 64u + 4u * j;
-      W[j] = (tail_byte(tail, rem, o, nblk, bits) << 24) | (tail_byte(tail, rem, o + 1, nblk, bits) << 16) |
-             (tail_byte(tail, rem, o + 2, nblk, bits) << 8) | tail_byte(tail, rem, o + 3, nblk, bits);
-    }
-    compress(h, W);
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t o = tb * 64u + 4u * j;
+    W[j] = (tail_byte(tail, rem, o, nblk, bits) << 24) | (tail_byte(tail, rem, o + 1, nblk, bits) << 16) |
+           (tail_byte(tail, rem, o + 2, nblk, bits) << 8) | tail_byte(tail, rem, o + 3, nblk, bits);
   }
-  uint4* d = reinterpret_cast<uint4*>(digests + 32 * static_cast<int64_t>(i));
-  d[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
-  d[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
+}
+
+__device__ __forceinline__ uint64_t blocks_of(uint64_t len) {
+  return (len >> 6) + (((len & 63) + 9u <= 64u) ? 1u : 2u);
+}
+
+// Workgroup = 2 waves over the same 64 messages (lane = message).  A lone
+// wave issues about one instruction per ~5.5 cycles, so each message's chain
+// is issue-bound: the 64 rounds stay on wave 0 (14 instructions per round
+// with K+W precomputed), while wave 1 loads, byte-swaps and expands the
+// schedule of the NEXT block (~560 instructions) and hands K+W over through
+// a double-buffered LDS ring ([t/4][lane][4] u32: ds_*_b128, conflict-free).
+// One barrier per block.  Lanes whose message has fewer blocks idle (exec).
+constexpr int kShaLanes = 64;
+__global__ __launch_bounds__(128) void sha256_pair_kernel(const uint8_t* const* __restrict__ msgs,
+                                                          const uint64_t* __restrict__ lens, int k,
+                                                          uint8_t* __restrict__ digests) {
+  __shared__ __attribute__((aligned(16))) u32x4 ring[2][16][kShaLanes];
+  const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * kShaLanes + lane;
+  const bool live = i < k;
+  const uint8_t* m = live ? ldg(msgs + i) : nullptr;
+  const uint64_t len = live ? ldg(lens + i) : 0;
+  const uint64_t nb = live ? blocks_of(len) : 0;
+  // wave-uniform block count: max over the 64 lanes (same in both waves)
+  uint64_t nmax = nb;
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const uint32_t lo = __shfl_xor(static_cast<uint32_t>(nmax), s, 64);
+    const uint32_t hi = __shfl_xor(static_cast<uint32_t>(nmax >> 32), s, 64);
+    const uint64_t o = (static_cast<uint64_t>(hi) << 32) | lo;
+    nmax = o > nmax ? o : nmax;
+  }
+  nmax = uniform_u64(nmax);
+  const bool al16 = (reinterpret_cast<uintptr_t>(m) & 15) == 0;
+
+  if (wi == 1) {  // schedule wave: block j+1 while wave 0 compresses block j
+    for (uint64_t j = 0; j < nmax; ++j) {
+      if (j < nb) {
+        uint32_t W[64];
+        load_block(W, m, len, j, al16);
+        schedule_kw(W);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) ring[j & 1][q][lane] = u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]};
+      }
+      __syncthreads();  // block j is in the ring
+      __syncthreads();  // wave 0 has read it: fill block j+1 while wave 0 compresses block j
+    }
+    return;
+  }
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  for (uint64_t j = 0; j < nmax; ++j) {
+    __syncthreads();  // block j is in the ring
+    uint32_t kw[64];
+    if (j < nb) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const u32x4 x = ring[j & 1][q][lane];
+        kw[4 * q] = x.x; kw[4 * q + 1] = x.y; kw[4 * q + 2] = x.z; kw[4 * q + 3] = x.w;
+      }
+    }
+    __syncthreads();  // slot j&1 read: wave 1 may refill it with block j+2
+    if (j < nb) rounds_kw(h, kw);
+  }
+  if (live) {
+    uint4* d = reinterpret_cast<uint4*>(digests + 32 * static_cast<int64_t>(i));
+    d[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
+    d[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
+  }
 }
 
 // Order-preserving compaction of accepted payload pointers (single block).
@@ -154,7 +222,7 @@ extern "C" int32_t p2p_sha256_batch(const uint8_t* const* msgs, const uint64_t* 
   if (!msgs || !lens || !digests || k < 0) return P2P_ERR_INVALID;
   if (reinterpret_cast<uintptr_t>(digests) & 15) return P2P_ERR_ALIGN;
   if (k == 0) return P2P_OK;
-  hipLaunchKernelGGL(sha256_batch_kernel, dim3((k + 63) / 64), dim3(64), 0,
+  hipLaunchKernelGGL(sha256_pair_kernel, dim3((k + kShaLanes - 1) / kShaLanes), dim3(128), 0,
                      static_cast<hipStream_t>(stream), msgs, lens, k, digests);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? P2P_OK : static_cast<int32_t>(e);

@@ -19,6 +19,7 @@
 template <int MODE>
 __global__ __launch_bounds__(256) void k(uint32_t* out, int reps) {
   uint32_t r = threadIdx.x;
+  if (MODE >= 20 && (threadIdx.x & 63) >= (MODE == 20 ? 32 : 16)) return;  // half / quarter wave
   for (int i = 0; i < reps; ++i) {
     if constexpr (MODE == 0) {  // second operand v20 (bank 0) vs first operands v8..v15 (banks 0..3)
       asm volatile(BODY(20) BODY(20) BODY(20) BODY(20) ::: "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
@@ -46,7 +47,9 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, int reps) {
             "v_mov_b32_dpp v46, v10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n v_mov_b32_dpp v47, v11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n "
 #define OPB(OP) OP " v40, v8, v9\n " OP " v41, v9, v10\n " OP " v42, v10, v11\n " OP " v43, v11, v12\n " \
                 OP " v44, v8, v9\n " OP " v45, v9, v10\n " OP " v46, v10, v11\n " OP " v47, v11, v12\n "
-      if constexpr (MODE == 3)
+      if constexpr (MODE >= 20)
+        asm volatile(OPB("v_xor_b32") OPB("v_add_u32") OPB("v_xor_b32") OPB("v_add_u32") ::: "v8", "v9", "v10", "v11", "v12", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
+      else if constexpr (MODE == 3)
         asm volatile(OPB("v_mul_f32") OPB("v_mul_f32") OPB("v_mul_f32") OPB("v_mul_f32") ::: "v8", "v9", "v10", "v11", "v12", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
       else if constexpr (MODE == 4)
         asm volatile(OPB("v_xor_b32") OPB("v_xor_b32") OPB("v_xor_b32") OPB("v_xor_b32") ::: "v8", "v9", "v10", "v11", "v12", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
@@ -102,6 +105,11 @@ static void run(const char* tag, uint32_t* out, int waves_per_simd) {
 int main() {
   uint32_t* out;
   CHECK(hipMalloc(&out, 256 * 1024 * 8 * 4));
+  for (int w : {1, 2}) {
+    run<4>("xor/add full wave", out, w);
+    run<20>("xor/add 32 lanes", out, w);
+    run<21>("xor/add 16 lanes", out, w);
+  }
   for (int w : {2, 4}) {
     run<2>("min/max u32", out, w);
     run<3>("v_mul_f32", out, w);
