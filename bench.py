@@ -183,7 +183,7 @@ def run_digest_workload(args, rule, K, n, seed, dev):
                      "fedavg_gbs": round(agg_bytes / (agg_ms / 1e3) / 1e9, 1) if agg_bytes else None,
                      # serial-chain issue bound: one wave issues ~1 instruction / 4 cycles at
                      # 2.4 GHz, ~910 instructions per 64-B block on the chain
-                     "chain_issue_bound_gbs": round(min(K, 1024) * 64 / (910 * 4 / 2.4e9) / 1e9, 2)},
+                     "chain_issue_bound_gbs": round(min(K, 65536) * 64 / (910 * 4 / 2.4e9) / 1e9, 2)},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
