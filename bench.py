@@ -52,6 +52,9 @@ WORKLOADS = {
     "sha256": ("sha256", 256, 25_000_000, 0x5EED0004),
     # trainer-side delta + snapshot of cfg3's 1B-param model
     "delta": ("delta", 1, 1_000_000_000, 0x5EED0006),
+    # cfg1: the reference's default run -- MNIST MLP (models/model.py:6-8), 3
+    # peers, the drop-in aggregate_models end to end (latency-bound)
+    "cfg1": ("dropin", 3, 535_818, 0x5EED0000),
 }
 MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
@@ -251,6 +254,82 @@ def run_delta_workload(args, n, seed, dev):
         "cpu_baseline": cpu}), flush=True)
 
 
+MLP_SHAPES = [("fc1.weight", (512, 784)), ("fc1.bias", (512,)), ("fc2.weight", (256, 512)),
+              ("fc2.bias", (256,)), ("fc3.weight", (10, 256)), ("fc3.bias", (10,))]  # models/model.py:6-8
+
+
+def run_dropin_workload(args, K, seed, dev):
+    """cfg1: one call of the drop-in aggregate_models (reference
+    aggregator/aggregation.py:7-46) on the MNIST MLP with K updates, host
+    table building included -- latency, reported as us per call."""
+    import types
+
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    agg_bc = agg.broadcast_global_model_update
+    agg.broadcast_global_model_update = lambda self: None  # networking is out of scope
+    model = torch.nn.Module()
+    n = 0
+    for name, shape in MLP_SHAPES:
+        mod, attr = name.split(".")
+        if not hasattr(model, mod):
+            model.add_module(mod, torch.nn.Module())
+        t = torch.empty(shape, dtype=torch.float32, device=dev)
+        ops.fill_synthetic_(t.view(-1), seed, W_PEER, W_SCALE)
+        getattr(model, mod).register_parameter(attr, torch.nn.Parameter(t, requires_grad=False))
+        n += t.numel()
+    updates = []
+    for p in range(K):
+        upd = {}
+        for name, shape in MLP_SHAPES:
+            t = torch.empty(shape, dtype=torch.float32, device=dev)
+            ops.fill_synthetic_(t.view(-1), seed, p, UPD_SCALE)
+            upd[name] = t
+        updates.append(upd)
+    node = types.SimpleNamespace(model=model, trainers_list=[0] * K, addr="127.0.0.1", port=1, neighbors=[],
+                                 received_models=[])
+
+    def call():
+        node.received_models.extend({"model": u, "sender": j} for j, u in enumerate(updates))
+        agg.aggregate_models(node)
+
+    for _ in range(max(args.warmup, 3)):
+        call()
+    torch.cuda.synchronize()
+    steps = max(args.steps, 100)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        call()
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / steps * 1e6
+    agg.broadcast_global_model_update = agg_bc
+    cpu = None
+    if not args.no_cpu_baseline:
+        import oracle.cpu_baseline as cb  # baseline leg only
+
+        torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+        ws = [torch.zeros(s) for _, s in MLP_SHAPES]
+        peers = [[torch.rand(s) for _, s in MLP_SHAPES] for _ in range(K)]
+        reps, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < min(args.cpu_seconds, 3.0):
+            for l, w in enumerate(ws):  # the reference's per-key op sequence (aggregation.py:15-38)
+                cb.reference_ops_fedavg_(w, [p[l] for p in peers])
+            reps += 1
+        cus = (time.perf_counter() - t1) / reps * 1e6
+        cpu = {"value": round(cus, 1), "unit": "us per aggregation", "cores": torch.get_num_threads(),
+               "kind": "port", "sample": f"MLP state_dict ({n:,} params) x {K} updates, reference op sequence "
+                                         f"per key on torch CPU, {reps} reps"}
+    print(json.dumps({
+        "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
+        "value": round(K * n * 4 / (us * 1e-6) / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": round(us / 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic MLP weights and updates (device PRNG)",
+        "config": {"workload": f"cfg1: drop-in aggregate_models, MNIST MLP ({n:,} params) x {K} updates, "
+                               f"latency-bound (us_per_call)", "us_per_call": round(us, 1),
+                   "parallelism": "single GPU"},
+        "roofline": None, "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -281,6 +360,10 @@ def main():
         if world > 1:
             raise SystemExit("delta runs as replicas only (one process per GPU)")
         return run_delta_workload(args, n, seed, dev)
+    if rule == "dropin":
+        if world > 1:
+            raise SystemExit("cfg1 runs on one GPU")
+        return run_dropin_workload(args, K, seed, dev)
     S = args.chunks if world > 1 else 1
     C = -(-n // S)
     n = C * S  # whole chunks per rank
@@ -396,9 +479,10 @@ def main():
             gbs, thr, reps, el = cb.time_fedavg(K, n_s, args.cpu_seconds)
         else:
             gbs, thr, reps, el = cb.time_median(K, n_s, args.cpu_seconds)
+        what = ("reference op sequence (aggregation.py:15-38)" if rule == "fedavg"
+                else "torch.median(dim=0) (the build-defined rule on CPU)")
         cpu = {"value": round(gbs, 3), "unit": "GB/s", "cores": thr, "kind": "port",
-               "sample": f"{K} peers x {n_s:,} fp32 coords, reference op sequence "
-                         f"(aggregation.py:15-38) on torch CPU, {reps} reps in {el:.1f}s"}
+               "sample": f"{K} peers x {n_s:,} fp32 coords, {what} on torch CPU, {reps} reps in {el:.1f}s"}
 
     if rank == 0:
         line = {
