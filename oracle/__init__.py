@@ -103,6 +103,16 @@ def synth_np(n: int, seed: int, peer: int, scale: float, chunk: int = 0, nranks:
     return x * np.float32(scale)
 
 
+def synth_at(idx, seed: int, peer: int, scale: float) -> np.ndarray:
+    """The PRNG at arbitrary global coordinates (size-independent checks of
+    buffers too large to regenerate on the host)."""
+    i = np.asarray(idx, dtype=np.int64)
+    with np.errstate(over="ignore"):
+        u = _splitmix64_np(np.uint64(seed) ^ (np.uint64(peer) << np.uint64(40)) ^ i.astype(np.uint64))
+    u = (u >> np.uint64(40)).astype(np.float32)
+    return (u * np.float32(2.0 ** -23) - np.float32(1.0)) * np.float32(scale)
+
+
 # ---------------------------------------------------------------- FedAvg
 def fedavg(peers, w=None, lr: float = 0.1, want_out: bool = False):
     """C restatement of reference aggregator/aggregation.py:15-38.

@@ -11,22 +11,25 @@
 // element once, keeps the running sum in VGPRs and touches w once:
 // algorithmic bytes = 4*n*(K+2) per launch (K peer reads + w read + w write).
 //
-// Layout (measured, tools/fedavg_sweep.hip): a 256-lane block owns a
-// 4096-float tile; lane l owns the float4s at l, l+256, l+512, l+768 of it,
-// so EVERY load instruction reads one contiguous 1 KB per wave (a lane-
+// Layout (measured, tools/fedavg_sweep.hip): a 256-lane block owns a tile
+// of NV x 1024 floats; lane l owns the float4s at l, l+256, ... of it, so
+// EVERY load instruction reads one contiguous 1 KB per wave (a lane-
 // contiguous 32-B layout halves the useful bytes per instruction and ran at
-// 61-73% of peak).  The peer loop is unrolled 8 deep (32 x 16-B loads in
-// flight per lane), peer streams use nontemporal loads (read once), one tile
-// per block.  128 GB cfg3 tile: 6.18 TB/s = 77% of 8 TB/s.  No inter-block
-// reuse exists, so no XCD remap is needed (guide T1: 0% on elementwise).
+// 61-73% of peak).  The peer loop is unrolled 8 deep, peer streams use
+// nontemporal loads (read once), one tile per block.  128 GB cfg3 tile:
+// 6.2-6.4 TB/s = 78-80% of 8 TB/s.  No inter-block reuse exists, so no XCD
+// remap is needed (guide T1: 0% on elementwise).
+#include <stdlib.h>
+
 #include "p2p_common.h"
 
 namespace p2p {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kNV = 4;                    // float4s per lane per tile
+constexpr int kNV = 4;                    // float4s per lane per tile (segment kernel)
 constexpr int kTile = kBlock * 4 * kNV;   // 4096 floats per tile
+template <int NV> constexpr int tile_of() { return kBlock * 4 * NV; }
 constexpr int kUnroll = 8;
 
 __device__ __forceinline__ f4 ld_nt(const float* p) { return ldg_nt(reinterpret_cast<const f4*>(p)); }
@@ -50,40 +53,40 @@ __device__ __forceinline__ f4 apply4(f4 w, float lr, f4 m) {
 // complete float4 groups still use vector loads under a per-lane predicate;
 // the <= 3 trailing elements of the array go element by element.  Same op
 // order on every path.
-template <bool FULL>
+template <int NV, bool FULL>
 __device__ __forceinline__ void fedavg_tile_vec(const float* const* __restrict__ peers, int K,
                                                 int64_t n, int64_t base, float* w, float* out,
                                                 float lr) {
   const float fk = static_cast<float>(K);
-  bool ok[kNV];
+  bool ok[NV];
 #pragma unroll
-  for (int v = 0; v < kNV; ++v) ok[v] = FULL || (base + kBlock * 4 * v + 4 <= n);
-  f4 acc[kNV];
+  for (int v = 0; v < NV; ++v) ok[v] = FULL || (base + kBlock * 4 * v + 4 <= n);
+  f4 acc[NV];
 #pragma unroll
-  for (int v = 0; v < kNV; ++v) acc[v] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
+  for (int v = 0; v < NV; ++v) acc[v] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
   int k = 0;
   for (; k + kUnroll <= K; k += kUnroll) {
-    f4 x[kUnroll][kNV];
+    f4 x[kUnroll][NV];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const float* p = table_at(peers, k + u) + base;
 #pragma unroll
-      for (int v = 0; v < kNV; ++v)
+      for (int v = 0; v < NV; ++v)
         x[u][v] = ok[v] ? ld_nt(p + kBlock * 4 * v) : f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)  // strictly in list order (:25-28)
 #pragma unroll
-      for (int v = 0; v < kNV; ++v) acc[v] += x[u][v];
+      for (int v = 0; v < NV; ++v) acc[v] += x[u][v];
   }
   for (; k < K; ++k) {
     const float* p = table_at(peers, k) + base;
 #pragma unroll
-    for (int v = 0; v < kNV; ++v)
+    for (int v = 0; v < NV; ++v)
       acc[v] += ok[v] ? ld_nt(p + kBlock * 4 * v) : f4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
-  for (int v = 0; v < kNV; ++v) {
+  for (int v = 0; v < NV; ++v) {
     if (!ok[v]) continue;
     const int64_t o = base + kBlock * 4 * v;
     const f4 m = div4(acc[v], fk);  // (:31-32)
@@ -103,19 +106,20 @@ __device__ __forceinline__ void fedavg_elem(const float* const* __restrict__ pee
   if (w) stg(w + i, apply_lr(ldg(w + i), lr, m));
 }
 
+template <int NV>
 __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ peers, int K,
                                             int64_t n, int64_t tile0, float* w, float* out,
                                             float lr, bool aligned) {
   const int64_t base = tile0 + 4 * static_cast<int64_t>(threadIdx.x);
   if (aligned) {
-    if (tile0 + kTile <= n) {
-      fedavg_tile_vec<true>(peers, K, n, base, w, out, lr);
+    if (tile0 + tile_of<NV>() <= n) {
+      fedavg_tile_vec<NV, true>(peers, K, n, base, w, out, lr);
       return;
     }
-    fedavg_tile_vec<false>(peers, K, n, base, w, out, lr);
+    fedavg_tile_vec<NV, false>(peers, K, n, base, w, out, lr);
     // trailing elements of a float4 group that straddles n
 #pragma unroll 1
-    for (int v = 0; v < kNV; ++v) {
+    for (int v = 0; v < NV; ++v) {
       const int64_t g = base + kBlock * 4 * v;
       if (g < n && g + 4 > n)
         for (int64_t i = g; i < n; ++i) fedavg_elem(peers, K, i, w, out, lr);
@@ -123,7 +127,7 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
     return;
   }
 #pragma unroll 1
-  for (int v = 0; v < kNV; ++v)
+  for (int v = 0; v < NV; ++v)
 #pragma unroll 1
     for (int e = 0; e < 4; ++e) {
       const int64_t i = base + kBlock * 4 * v + e;
@@ -133,6 +137,7 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
 
 // Flat buffer, one tile per block.  K either from the kernarg or, when
 // k_dev != nullptr, from device memory (fused accept -> FedAvg path).
+template <int NV>
 __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const* __restrict__ peers,
                                                              int K, const int32_t* k_dev,
                                                              int64_t n, float* w, float* out,
@@ -140,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const*
   if (k_dev) K = *k_dev;
   if (K <= 0) return;
   const bool aligned = all_aligned16(peers, K, w, out);
-  fedavg_tile(peers, K, n, static_cast<int64_t>(blockIdx.x) * kTile, w, out, lr, aligned);
+  fedavg_tile<NV>(peers, K, n, static_cast<int64_t>(blockIdx.x) * tile_of<NV>(), w, out, lr, aligned);
 }
 
 // Whole state_dict: one tile per block, segment found by binary search.
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void fedavg_segments_kernel(const Seg* __re
   const int64_t t = blockIdx.x;
   const Seg s = load_segment(segs, nseg, t);
   const bool aligned = all_aligned16(s.peers, K, s.w, s.out);
-  fedavg_tile(s.peers, K, s.n, (t - s.tile_begin) * kTile, s.w, s.out, lr, aligned);
+  fedavg_tile<kNV>(s.peers, K, s.n, (t - s.tile_begin) * kTile, s.w, s.out, lr, aligned);
 }
 
 __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* agg, float lr,
@@ -166,6 +171,38 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* ag
 }
 
 static int grid_for_tiles(int64_t ntiles) { return static_cast<int>(ntiles > 0 ? ntiles : 1); }
+
+// Flat launches use 1024-float tiles (one float4 per lane per peer, 8 peers
+// of loads in flight, 56 VGPRs -> full occupancy).  Measured against 4096:
+// cfg2 (64 x 11.7M) 76.8% vs 71.4% of HBM peak -- 2854 tiles of 4096 leave
+// the last wave of blocks part-empty -- and cfg3 (256 x 125M) 77.9% vs
+// 77.1%.  P2P_FEDAVG_NV forces 1, 2 or 4 (A/B).
+static int flat_nv(int64_t n) {
+  static const int forced = [] {
+    const char* e = getenv("P2P_FEDAVG_NV");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 1 || forced == 2 || forced == 4) return forced;
+  (void)n;
+  return 1;
+}
+
+static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,
+                        float lr, hipStream_t stream) {
+  switch (flat_nv(n)) {
+    case 1:
+      hipLaunchKernelGGL(fedavg_flat_kernel<1>, dim3(grid_for_tiles(ceil_div(n, tile_of<1>()))), dim3(kBlock), 0,
+                         stream, peers, K, k_dev, n, w, out, lr);
+      break;
+    case 2:
+      hipLaunchKernelGGL(fedavg_flat_kernel<2>, dim3(grid_for_tiles(ceil_div(n, tile_of<2>()))), dim3(kBlock), 0,
+                         stream, peers, K, k_dev, n, w, out, lr);
+      break;
+    default:
+      hipLaunchKernelGGL(fedavg_flat_kernel<4>, dim3(grid_for_tiles(ceil_div(n, tile_of<4>()))), dim3(kBlock), 0,
+                         stream, peers, K, k_dev, n, w, out, lr);
+  }
+}
 
 static int grid_stride_blocks(int64_t nblocks) {
   const int64_t cap = 256 * 8;  // 256 CUs x 8 resident blocks; grid-stride beyond
@@ -185,8 +222,7 @@ extern "C" P2P_INTERNAL int64_t p2p_fedavg_tile_elems(void) { return kTile; }
 
 P2P_INTERNAL int32_t p2p_fedavg_flat_launch(const float* const* peers, int32_t k, int64_t n, float* w,
                                             float* out, float lr, p2p_stream_t stream) {
-  hipLaunchKernelGGL(fedavg_flat_kernel, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), peers, k, nullptr, n, w, out, lr);
+  launch_flat(peers, k, nullptr, n, w, out, lr, static_cast<hipStream_t>(stream));
   return launch_status();
 }
 
@@ -195,8 +231,7 @@ extern "C" int32_t p2p_fedavg_apply_f32(const float* const* peers, int32_t k, in
   if (!peers || !w || k < 1 || n < 0) return P2P_ERR_INVALID;
   if (reinterpret_cast<uintptr_t>(w) & 3) return P2P_ERR_ALIGN;
   if (n == 0) return P2P_OK;
-  hipLaunchKernelGGL(fedavg_flat_kernel, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), peers, k, nullptr, n, w, nullptr, lr);
+  launch_flat(peers, k, nullptr, n, w, nullptr, lr, static_cast<hipStream_t>(stream));
   return launch_status();
 }
 
@@ -205,8 +240,7 @@ extern "C" int32_t p2p_mean_f32(const float* const* peers, int32_t k, int64_t n,
   if (!peers || !out || k < 1 || n < 0) return P2P_ERR_INVALID;
   if (reinterpret_cast<uintptr_t>(out) & 3) return P2P_ERR_ALIGN;
   if (n == 0) return P2P_OK;
-  hipLaunchKernelGGL(fedavg_flat_kernel, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), peers, k, nullptr, n, nullptr, out, 0.f);
+  launch_flat(peers, k, nullptr, n, nullptr, out, 0.f, static_cast<hipStream_t>(stream));
   return launch_status();
 }
 
@@ -216,8 +250,7 @@ extern "C" int32_t p2p_fedavg_apply_devk_f32(const float* const* peers, const in
   if (!peers || !k_dev || (!w && !out) || k_max < 1 || n < 0) return P2P_ERR_INVALID;
   if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(out)) & 3) return P2P_ERR_ALIGN;
   if (n == 0) return P2P_OK;
-  hipLaunchKernelGGL(fedavg_flat_kernel, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), peers, k_max, k_dev, n, w, out, lr);
+  launch_flat(peers, k_max, k_dev, n, w, out, lr, static_cast<hipStream_t>(stream));
   return launch_status();
 }
 

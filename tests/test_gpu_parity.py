@@ -318,6 +318,62 @@ def test_dropin_robust_rules(cuda, rule, k, monkeypatch):
     assert_bits_equal(out, w_ref, what=f"dropin {rule}")
 
 
+# ------------------------------------------------------------------ beyond 2**31 elements
+BIG_N = (1 << 31) + 37  # > 2**31 elements per buffer: 64-bit index math everywhere
+
+
+def _big_sample(n):
+    rng = np.random.default_rng(7)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 4000), np.arange(4096), n - 1 - np.arange(4096),
+                                    (1 << 31) - 2 + np.arange(8)]))
+    return idx[(idx >= 0) & (idx < n)]
+
+
+@pytest.mark.parametrize("rule", ["fedavg", "median", "trimmed"])
+def test_aggregate_beyond_2g_elements_sampled(cuda, rule):
+    """Full-size property check: every rule over K=3 peers of 2**31+37 fp32
+    (8.6 GB each), compared with the oracle on sampled coordinates incl. both
+    ends and the 2**31 boundary."""
+    k, n, seed = 3, BIG_N, 0x5EED00B1
+    peers = [torch.empty(n, dtype=torch.float32, device=cuda) for _ in range(k)]
+    for p, t in enumerate(peers):
+        ops.fill_synthetic_(t, seed, p, 1e-2)
+    w = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.fill_synthetic_(w, seed, 0xFFFFF, 5e-2)
+    ops.aggregate(peers, rule, w=w, lr=0.1)
+    idx = _big_sample(n)
+    got = w[torch.from_numpy(idx).to(cuda)].cpu().numpy()
+    x = [oracle.synth_at(idx, seed, p, 1e-2) for p in range(k)]
+    w0 = oracle.synth_at(idx, seed, 0xFFFFF, 5e-2)
+    if rule == "fedavg":
+        want, _ = oracle.fedavg(x, w0)
+    else:
+        r = ops.rule_id(rule)
+        want, _ = oracle.robust(x, r, ops.trim_count(k) if r == 2 else 0, w=w0)
+    del peers, w
+    torch.cuda.empty_cache()
+    assert_bits_equal(got, want, what=f"{rule} n=2**31+37")
+
+
+def test_delta_beyond_2g_elements_sampled(cuda):
+    n, seed = BIG_N, 0x5EED00B2
+    cur = torch.empty(n, dtype=torch.float32, device=cuda)
+    prev = torch.empty_like(cur)
+    ops.fill_synthetic_(cur, seed, 1, 1e-1)
+    ops.fill_synthetic_(prev, seed, 2, 1e-1)
+    delta = torch.empty_like(cur)
+    ops.delta_snapshot_(cur, prev, delta)
+    idx = _big_sample(n)
+    ti = torch.from_numpy(idx).to(cuda)
+    got_d, got_p = delta[ti].cpu().numpy(), prev[ti].cpu().numpy()
+    c, p = oracle.synth_at(idx, seed, 1, 1e-1), oracle.synth_at(idx, seed, 2, 1e-1)
+    want_d, want_p = oracle.delta_snapshot_np(c, p)
+    del cur, prev, delta
+    torch.cuda.empty_cache()
+    assert_bits_equal(got_d, want_d, what="delta n=2**31+37")
+    assert_bits_equal(got_p, want_p, what="snapshot n=2**31+37")
+
+
 # ------------------------------------------------------------------ K4 trainer delta
 @pytest.mark.parametrize("n", [1, 3, 4096, 4097, 100_003])
 @pytest.mark.parametrize("first", [False, True])

@@ -100,3 +100,9 @@ def test_delta_snapshot_oracle_matches_torch_reference_ops():
     assert np.array_equal(p, cur)
     d0, p0 = oracle.delta_snapshot_np(cur, None)
     assert np.array_equal(d0, cur) and np.array_equal(p0, cur) and d0 is not cur
+
+
+def test_synth_at_matches_synth():
+    idx = np.array([0, 1, 17, 4095, 99_999])
+    full = oracle.synth(100_000, 0x5EED0001, 3, 1e-2)
+    assert np.array_equal(oracle.synth_at(idx, 0x5EED0001, 3, 1e-2), full[idx])
