@@ -55,6 +55,9 @@ WORKLOADS = {
     # cfg1: the reference's default run -- MNIST MLP (models/model.py:6-8), 3
     # peers, the drop-in aggregate_models end to end (latency-bound)
     "cfg1": ("dropin", 3, 535_818, 0x5EED0000),
+    # land 16 serialized ResNet-18-sized updates (11.7M
+    # params each) in the device slab vs the reference's pickle.loads
+    "inbox": ("inbox", 16, 11_689_512, 0x5EED0007),
 }
 MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
@@ -330,6 +333,82 @@ def run_dropin_workload(args, K, seed, dev):
         "roofline": None, "cpu_baseline": cpu}), flush=True)
 
 
+def _resnet18_like_shapes(total):
+    """Tensor sizes of a ResNet-18 state_dict (conv/fc weights, BN vectors),
+    the last one padded so the parameters add up to `total`."""
+    sizes = [64 * 3 * 49] + [64] * 2 + [64 * 64 * 9] * 4 + [64] * 8 + [128 * 64 * 9, 128 * 128 * 9, 128 * 64]
+    sizes += [128 * 128 * 9] * 2 + [128] * 10 + [256 * 128 * 9, 256 * 256 * 9, 256 * 128] + [256 * 256 * 9] * 2
+    sizes += [256] * 10 + [512 * 256 * 9, 512 * 512 * 9, 512 * 256] + [512 * 512 * 9] * 2 + [512] * 10
+    sizes += [1000 * 512, 1000]
+    sizes[-2] += total - sum(sizes)
+    return sizes
+
+
+def run_inbox_workload(args, K, n, seed, dev):
+    """Receive path (reference node/node.py:135-138): K serialized updates of
+    a GPU sender (pickle of CUDA tensors, node/node.py:285) deserialized into
+    device tensors -- the reference's pickle.loads vs DeviceInbox.land.
+    value = update bytes landed per second (host-to-device, PCIe-bound)."""
+    import pickle
+
+    from p2pdl_amd.node.inbox import DeviceInbox
+
+    sizes = _resnet18_like_shapes(n)
+    keys = [f"layer{i}.weight" for i in range(len(sizes))]
+    ser = []
+    for p in range(K):
+        upd = {}
+        for i, (k, m) in enumerate(zip(keys, sizes)):
+            t = torch.empty(m, dtype=torch.float32, device=dev)
+            ops.fill_synthetic_(t, seed, p * 1000 + i, UPD_SCALE)
+            upd[k] = t
+        ser.append(pickle.dumps(upd))  # what a CUDA trainer sends
+    template = {k: torch.empty(m, dtype=torch.float32, device=dev) for k, m in zip(keys, sizes)}
+    inbox = DeviceInbox(template, k_max=K, device=dev)
+    if not args.no_check:
+        got = inbox.land(ser[0], 0)
+        ref = pickle.loads(ser[0])
+        torch.cuda.synchronize()
+        ok = all(torch.equal(got[k], ref[k]) for k in keys)
+        log(f"landed update == pickle.loads: {ok}")
+        if not ok:
+            raise SystemExit("bench: inbox differs from pickle.loads")
+
+    def timed(fn):
+        for _ in range(max(args.warmup, 1)):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / args.steps
+
+    def ours():
+        inbox.reset()
+        for s in ser:
+            inbox.land(s)
+
+    def reference():
+        for s in ser:
+            pickle.loads(s)
+
+    t_ours, t_ref = timed(ours), timed(reference)
+    nbytes = K * n * 4
+    print(json.dumps({
+        "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
+        "value": round(nbytes / t_ours / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(t_ours * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic ResNet-18-sized updates pickled from CUDA tensors",
+        "config": {"workload": f"inbox: land {K} serialized updates of {n:,} params ({len(sizes)} tensors) "
+                               f"in the device slab (SURVEY §8(f) row 1)", "reference_pickle_loads_gbs":
+                   round(nbytes / t_ref / 1e9, 3), "reference_ms": round(t_ref * 1e3, 3),
+                   "parallelism": "single GPU, host-to-device"},
+        "roofline": {"bound": "pcie (host-to-device)", "achieved": round(nbytes / t_ours / 1e9, 2), "peak": 63.0,
+                     "unit": "GB/s", "frac": round(nbytes / t_ours / 1e9 / 63.0, 4), "traffic": None},
+        "cpu_baseline": None}), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -360,6 +439,10 @@ def main():
         if world > 1:
             raise SystemExit("delta runs as replicas only (one process per GPU)")
         return run_delta_workload(args, n, seed, dev)
+    if rule == "inbox":
+        if world > 1:
+            raise SystemExit("inbox runs on one GPU")
+        return run_inbox_workload(args, K, n, seed, dev)
     if rule == "dropin":
         if world > 1:
             raise SystemExit("cfg1 runs on one GPU")

@@ -11,12 +11,15 @@ allocates and copies every tensor to the GPU separately.
 Here:
   * ``recv_message`` reads the 4-byte length and ``recv_into`` one
     preallocated buffer (linear);
-  * ``UpdateParser`` decodes the serialized update WITHOUT executing it: a
-    restricted unpickler that knows only the tensor-rebuild and
-    storage-load callables torch emits and an OrderedDict, parsing the legacy
-    storage blobs itself (magic, header pickles, raw little-endian payload).
-    Anything else in the stream raises ``pickle.UnpicklingError`` -- unlike
-    the reference's ``pickle.loads`` on network bytes;
+  * ``ZeroCopyParser`` decodes the serialized update WITHOUT executing it: a
+    restricted stack machine over the opcodes torch emits (protocols 3-5)
+    that resolves only the tensor-rebuild / legacy-storage callables and
+    OrderedDict, parses the legacy storage blobs itself (magic, header
+    pickles, raw little-endian payload) and hands the payloads out as
+    memoryview slices of the message -- no copy.  Anything else in the stream
+    raises ``pickle.UnpicklingError`` -- unlike the reference's
+    ``pickle.loads`` on network bytes.  (``UpdateParser`` is the same
+    restriction on top of the C unpickler, which copies each payload once.)
   * ``DeviceInbox.land`` copies the fp32 tensors of one update into row k of a
     preallocated [K_max, N] fp32 slab on the GPU through a pinned staging row
     -- one host-to-device copy per update -- and returns a state_dict whose
@@ -28,6 +31,7 @@ this on torch-produced pickles of the reference's message shapes).
 """
 from __future__ import annotations
 
+import os
 import pickle
 import struct
 from collections import OrderedDict
@@ -187,6 +191,178 @@ class UpdateParser(pickle.Unpickler):
         return obj
 
 
+class _Mark:
+    pass
+
+
+_MARK = _Mark()
+
+
+class ZeroCopyParser:
+    """Restricted stack-machine reader for the pickled state_dict of a peer
+    update (pickle protocols 3-5, the opcodes torch emits for a dict of
+    tensors).  Byte strings are returned as memoryview slices of the message
+    buffer -- the tensor payloads are never copied by the parser -- and only
+    the globals of ``UpdateParser`` resolve; anything else raises
+    ``pickle.UnpicklingError``."""
+
+    def __init__(self, data):
+        self.mv = memoryview(data).cast("B")
+
+    def parse(self) -> dict:
+        mv = self.mv
+        n = len(mv)
+        pos = 0
+        stack: list = []
+        memo: dict = {}
+        u8 = lambda p: mv[p]  # noqa: E731
+        le = lambda p, k: int.from_bytes(mv[p:p + k], "little")  # noqa: E731
+
+        def pop_mark():
+            nonlocal stack
+            for i in range(len(stack) - 1, -1, -1):
+                if stack[i] is _MARK:
+                    items = stack[i + 1:]
+                    stack = stack[:i]
+                    return items
+            raise pickle.UnpicklingError("MARK not found")
+
+        while pos < n:
+            op = mv[pos]
+            pos += 1
+            if op == 0x80:            # PROTO
+                if mv[pos] < 3:
+                    raise pickle.UnpicklingError(f"pickle protocol {mv[pos]} (< 3) is not accepted")
+                pos += 1
+            elif op == 0x95:          # FRAME (8-byte length; frames are inline)
+                pos += 8
+            elif op == 0x2E:          # STOP
+                result = stack.pop()
+                if not isinstance(result, dict) or not all(isinstance(v, RawTensor) for v in result.values()):
+                    raise pickle.UnpicklingError("a peer update must be a dict of tensors")
+                return result
+            elif op == 0x28:          # MARK
+                stack.append(_MARK)
+            elif op == 0x7D:          # EMPTY_DICT
+                stack.append({})
+            elif op == 0x29:          # EMPTY_TUPLE
+                stack.append(())
+            elif op == 0x5D:          # EMPTY_LIST
+                stack.append([])
+            elif op == 0x94:          # MEMOIZE
+                memo[len(memo)] = stack[-1]
+            elif op == 0x71:          # BINPUT
+                memo[mv[pos]] = stack[-1]
+                pos += 1
+            elif op == 0x72:          # LONG_BINPUT
+                memo[le(pos, 4)] = stack[-1]
+                pos += 4
+            elif op == 0x68:          # BINGET
+                stack.append(memo[mv[pos]])
+                pos += 1
+            elif op == 0x6A:          # LONG_BINGET
+                stack.append(memo[le(pos, 4)])
+                pos += 4
+            elif op == 0x8C:          # SHORT_BINUNICODE
+                k = mv[pos]
+                stack.append(str(mv[pos + 1:pos + 1 + k], "utf-8"))
+                pos += 1 + k
+            elif op == 0x58:          # BINUNICODE
+                k = le(pos, 4)
+                stack.append(str(mv[pos + 4:pos + 4 + k], "utf-8"))
+                pos += 4 + k
+            elif op == 0x43:          # SHORT_BINBYTES
+                k = mv[pos]
+                stack.append(mv[pos + 1:pos + 1 + k])
+                pos += 1 + k
+            elif op == 0x42:          # BINBYTES
+                k = le(pos, 4)
+                stack.append(mv[pos + 4:pos + 4 + k])
+                pos += 4 + k
+            elif op == 0x8E:          # BINBYTES8
+                k = le(pos, 8)
+                stack.append(mv[pos + 8:pos + 8 + k])
+                pos += 8 + k
+            elif op == 0x4B:          # BININT1
+                stack.append(mv[pos])
+                pos += 1
+            elif op == 0x4D:          # BININT2
+                stack.append(le(pos, 2))
+                pos += 2
+            elif op == 0x4A:          # BININT (signed)
+                stack.append(int.from_bytes(mv[pos:pos + 4], "little", signed=True))
+                pos += 4
+            elif op == 0x8A:          # LONG1
+                k = mv[pos]
+                stack.append(int.from_bytes(mv[pos + 1:pos + 1 + k], "little", signed=True))
+                pos += 1 + k
+            elif op == 0x89:          # NEWFALSE
+                stack.append(False)
+            elif op == 0x88:          # NEWTRUE
+                stack.append(True)
+            elif op == 0x4E:          # NONE
+                stack.append(None)
+            elif op == 0x85:          # TUPLE1
+                stack[-1] = (stack[-1],)
+            elif op == 0x86:          # TUPLE2
+                b = stack.pop()
+                stack[-1] = (stack[-1], b)
+            elif op == 0x87:          # TUPLE3
+                c = stack.pop()
+                b = stack.pop()
+                stack[-1] = (stack[-1], b, c)
+            elif op == 0x74:          # TUPLE
+                items = pop_mark()  # rebinds `stack`: take the items first
+                stack.append(tuple(items))
+            elif op == 0x93:          # STACK_GLOBAL
+                name = stack.pop()
+                module = stack.pop()
+                stack.append(self._global(module, name))
+            elif op == 0x63:          # GLOBAL (text: module\nname\n)
+                e1 = bytes(mv[pos:pos + 256]).index(b"\n")
+                module = str(mv[pos:pos + e1], "ascii")
+                e2 = bytes(mv[pos + e1 + 1:pos + e1 + 257]).index(b"\n")
+                name = str(mv[pos + e1 + 1:pos + e1 + 1 + e2], "ascii")
+                pos += e1 + e2 + 2
+                stack.append(self._global(module, name))
+            elif op == 0x52:          # REDUCE
+                args = stack.pop()
+                fn = stack[-1]
+                stack[-1] = fn(*args)
+            elif op == 0x62:          # BUILD (OrderedDict metadata: set attributes)
+                state = stack.pop()
+                inst = stack[-1]
+                if isinstance(state, dict) and isinstance(inst, OrderedDict):
+                    inst.__dict__.update({k: v for k, v in state.items() if isinstance(k, str)})
+                elif state is not None:
+                    raise pickle.UnpicklingError("unexpected BUILD")
+            elif op == 0x73:          # SETITEM
+                v = stack.pop()
+                k = stack.pop()
+                stack[-1][k] = v
+            elif op == 0x75:          # SETITEMS
+                items = pop_mark()
+                d = stack[-1]
+                for i in range(0, len(items), 2):
+                    d[items[i]] = items[i + 1]
+            elif op == 0x61:          # APPEND
+                v = stack.pop()
+                stack[-1].append(v)
+            elif op == 0x65:          # APPENDS
+                items = pop_mark()
+                stack[-1].extend(items)
+            else:
+                raise pickle.UnpicklingError(f"opcode 0x{op:02x} is not accepted in a peer update")
+        raise pickle.UnpicklingError("truncated pickle")
+
+    @staticmethod
+    def _global(module, name):
+        fn = UpdateParser._ALLOWED.get((module, name))
+        if fn is None:
+            raise pickle.UnpicklingError(f"refusing to load global {module}.{name} from a peer update")
+        return fn
+
+
 def recv_exact_into(conn, buf: memoryview) -> int:
     """Fill buf from the socket; returns the bytes received (< len on EOF)."""
     got = 0
@@ -244,8 +420,10 @@ class DeviceInbox:
     def land(self, serialized, k: int | None = None) -> dict:
         """Parse one serialized update and copy it to slab row k (next free row
         by default).  Returns {key: tensor} in the update's key order, fp32
-        entries as views of the slab row -- bit-identical to pickle.loads."""
-        raw = UpdateParser.parse(serialized)
+        entries as views of the slab row -- bit-identical to pickle.loads.
+        The payloads go message buffer -> pinned staging row (one memcpy,
+        split across a thread pool) -> device (one DMA)."""
+        raw = ZeroCopyParser(serialized).parse()
         if k is None:
             k = self.count
         if not 0 <= k < self.k_max:
@@ -257,15 +435,17 @@ class DeviceInbox:
         stage = self._stage[s].numpy()
         row = self.slab[k]
         out = OrderedDict()
+        jobs = []
         for key, rt in raw.items():
             lay = self.layout.get(key)
             if lay is not None and rt.storage.dtype is np.float32:
                 off, shape, n = lay
                 if rt.size != shape:
                     raise RuntimeError(f"update key {key}: shape {rt.size} != {shape}")
-                stage[off:off + n] = rt.array().reshape(-1)
+                jobs.append((stage[off:off + n], rt))
             else:  # not part of the fp32 slab: a small tensor of its own
                 out[key] = torch.from_numpy(np.array(rt.array())).to(self.device)
+        _copy_all(jobs)
         with torch.cuda.device(self.device):
             row.copy_(self._stage[s], non_blocking=True)
             ev = torch.cuda.Event()
@@ -277,3 +457,26 @@ class DeviceInbox:
             off, shape, n = self.layout[key]
             out[key] = row[off:off + n].view(shape)
         return OrderedDict((key, out[key]) for key in raw)
+
+
+_POOL = None
+
+
+def _copy_all(jobs) -> None:
+    """dst[:] = src for (dst, RawTensor) pairs; large copies on a thread pool
+    (numpy releases the GIL while copying)."""
+    global _POOL
+    big = [j for j in jobs if j[0].size >= (1 << 18)]
+    small = [j for j in jobs if j[0].size < (1 << 18)]
+    if big:
+        if _POOL is None:
+            from concurrent.futures import ThreadPoolExecutor
+            _POOL = ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1))
+        pieces = []
+        for dst, rt in big:  # split the large tensors into ~1M-element pieces
+            src = rt.array().reshape(-1)
+            for a in range(0, dst.size, 1 << 20):
+                pieces.append((dst[a:a + (1 << 20)], src[a:a + (1 << 20)]))
+        list(_POOL.map(lambda p: np.copyto(p[0], p[1]), pieces))
+    for dst, rt in small:
+        dst[:] = rt.array().reshape(-1)

@@ -16,7 +16,7 @@ import torch
 
 import oracle
 from helpers import assert_bits_equal
-from p2pdl_amd.node.inbox import DeviceInbox, UpdateParser, recv_message
+from p2pdl_amd.node.inbox import DeviceInbox, UpdateParser, ZeroCopyParser, recv_message
 
 MLP_SHAPES = [("fc1.weight", (512, 784)), ("fc1.bias", (512,)), ("fc2.weight", (256, 512)),
               ("fc2.bias", (256,)), ("fc3.weight", (10, 256)), ("fc3.bias", (10,))]  # models/model.py:6-8
@@ -38,19 +38,36 @@ def same(raw, ref):
         assert a.dtype == r.dtype and np.array_equal(a.view(np.uint8), r.view(np.uint8)), k
 
 
-def test_parser_matches_pickle_loads_mlp_update():
+PARSERS = [UpdateParser.parse, lambda d: ZeroCopyParser(d).parse()]
+
+
+@pytest.mark.parametrize("parse", PARSERS, ids=["c-unpickler", "zero-copy"])
+def test_parser_matches_pickle_loads_mlp_update(parse):
     upd = mlp_update(1)
     data = pickle.dumps(upd)  # reference node/node.py:285
-    same(UpdateParser.parse(data), pickle.loads(data))
+    same(parse(data), pickle.loads(data))
 
 
-def test_parser_batchnorm_scalars_views_and_ordereddict():
+@pytest.mark.parametrize("proto", [3, 4, 5])
+@pytest.mark.parametrize("parse", PARSERS, ids=["c-unpickler", "zero-copy"])
+def test_parser_batchnorm_scalars_views_and_ordereddict(parse, proto):
     net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.BatchNorm1d(5))
     sd = net.state_dict()  # OrderedDict incl. an int64 0-d buffer
     sd["view.t"] = torch.arange(12, dtype=torch.float32).reshape(3, 4).t()  # strided view
     sd["view.slice"] = torch.arange(20, dtype=torch.float32)[5:9]           # storage offset
-    data = pickle.dumps(sd)
-    same(UpdateParser.parse(data), pickle.loads(data))
+    sd["x" * 300] = torch.ones(3)                                           # BINUNICODE key
+    data = pickle.dumps(sd, protocol=proto)
+    same(parse(data), pickle.loads(data))
+
+
+def test_zero_copy_parser_payloads_alias_the_message():
+    data = bytearray(pickle.dumps({"w": torch.arange(1000, dtype=torch.float32)}))
+    raw = ZeroCopyParser(data).parse()
+    arr = raw["w"].array()
+    assert arr[7] == 7.0
+    i = bytes(data).index(np.arange(1000, dtype=np.float32)[5:9].tobytes())
+    data[i:i + 4] = np.float32(-1).tobytes()  # mutate the message: the view sees it
+    assert raw["w"].array()[5] == -1.0
 
 
 class _Evil:
@@ -65,8 +82,17 @@ class _Evil:
     {"a": 3},
 ])
 def test_parser_rejects_anything_but_tensors(payload):
+    for parse in PARSERS:
+        with pytest.raises(pickle.UnpicklingError):
+            parse(pickle.dumps(payload))
+
+
+def test_zero_copy_parser_rejects_protocol_2_and_truncation():
     with pytest.raises(pickle.UnpicklingError):
-        UpdateParser.parse(pickle.dumps(payload))
+        ZeroCopyParser(pickle.dumps({"a": torch.ones(2)}, protocol=2)).parse()
+    data = pickle.dumps({"a": torch.ones(2)})
+    with pytest.raises((pickle.UnpicklingError, IndexError, ValueError)):
+        ZeroCopyParser(data[:-20]).parse()
 
 
 def test_recv_message_framing_and_early_close():
