@@ -103,7 +103,7 @@ int32_t p2p_aggregate_segments_f32(const p2p_segment_t *segs, int32_t nseg, int6
  * kernel layout for robust rules with 65 <= k <= 256.  0 = default (fastest
  * measured per k), 1 = LDS-DMA staged 4 lanes per coordinate for every k,
  * 2 = same with 2 lanes x 64 keys at k <= 128, 3 = the one-lane / 4-wave
- * group kernels.  Results are identical; tile sizes (p2p_tile_elems) follow
+ * group kernels, 4 = one lane x 128 keys LDS-DMA staged at k <= 128.  Results are identical; tile sizes (p2p_tile_elems) follow
  * the layout, so segment tables must be built after choosing it. */
 int32_t p2p_set_robust_layout(int32_t layout);
 

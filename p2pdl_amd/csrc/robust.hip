@@ -443,13 +443,17 @@ extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, co
 //   1 "lds"    robust_lds.hip for every K in 65..256 (4 lanes x 32 keys at K <= 128)
 //   2 "lds2"   robust_lds.hip, 2 lanes x 64 keys at K <= 128
 //   3 "group"  this file only: one lane (K <= 128) / 4-wave LDS group (K > 128)
+//   4 "lds1"   robust_lds.hip, one lane x 128 keys (LDS-DMA staged) at K <= 128
+// (Measured and dropped: one LDS image per block with two blocks per CU for
+// K > 128 -- 2 sorter waves per SIMD -- ran the same 26.6 ms as one block
+// with two images: the K = 256 kernel is VALU-bound)
 static int g_robust_impl = -1;
 static int robust_impl() {
   if (g_robust_impl < 0) {
     const char* e = getenv("P2P_ROBUST_IMPL");
     int v = 0;
     if (e && e[0] == 'g') v = 3;
-    else if (e && e[0] == 'l' && e[1] == 'd' && e[2] == 's') v = (e[3] == '2') ? 2 : 1;
+    else if (e && e[0] == 'l' && e[1] == 'd' && e[2] == 's') v = (e[3] == '2') ? 2 : (e[3] == '1') ? 4 : 1;
     g_robust_impl = v;
   }
   return g_robust_impl;
@@ -459,11 +463,11 @@ static int robust_impl() {
 static int lds_variant(int k, int impl) {
   if (k <= 64 || impl == 3) return -1;
   if (k > 128) return 0;
-  return impl == 1 ? 0 : impl == 2 ? 1 : -1;
+  return impl == 1 ? 0 : impl == 2 ? 1 : impl == 4 ? 2 : -1;
 }
 
 extern "C" int32_t p2p_set_robust_layout(int32_t layout) {
-  if (layout < 0 || layout > 3) return P2P_ERR_INVALID;
+  if (layout < 0 || layout > 4) return P2P_ERR_INVALID;
   g_robust_impl = layout;
   return P2P_OK;
 }

@@ -7,8 +7,8 @@
 //            IEEE-divided by K-2b
 // then w += lr*agg, multiply and add separately rounded (aggregation.py:36-38).
 //
-// Layout.  A block of L waves owns a tile of 64 coordinates; wave wi takes
-// coordinates [16*wi*4/L ...) -- 64/L of them -- and lane = L*c + q holds
+// Layout.  A block's 4 sorter waves own a tile of 256/L coordinates; wave wi
+// takes coordinates [wi*64/L, (wi+1)*64/L) and lane = L*c + q holds
 // keys q*H .. q*H+H-1 (H = KP/L) of coordinate c, so every cross-lane step
 // is a DPP quad_perm inside a quad, never LDS.  Each lane sorts its H keys
 // in VGPRs (Batcher network), then the L slices are merged bitonically:
@@ -71,20 +71,24 @@ __device__ __forceinline__ float from_prev_slice(float x) {
   return __uint_as_float(dpp<L == 4 ? 0x90 : 0xA0>(__float_as_uint(x)));
 }
 
-template <int L, int H>
+template <int L, int H, int NB = 0>
 struct LdsLayout {
-  static constexpr int W = L;                  // waves per block
-  static constexpr int TB = 64;                // coordinates per block tile
-  static constexpr int TW = TB / W;            // coordinates per wave (= lanes / L)
-  static constexpr int RB = 4 * TB;            // bytes per peer row (256 contiguous in HBM)
+  static constexpr int W = 4;                  // sorter waves per block (and as many loaders)
+  static constexpr int TB = 64 * W / L;        // coordinates per block tile
+  static constexpr int TW = 64 / L;            // coordinates per sorter wave
+  static constexpr int RB = 4 * TB;            // bytes per peer row (>= 256 contiguous in HBM)
   static constexpr int PAD = L > 1 ? 128 / L : 0;
   static constexpr int SB = H * RB + PAD;      // bytes per slice
   static constexpr int WOFF = L * SB;          // w row
   static constexpr int IMG = (WOFF + RB + 15) / 16 * 16;  // one tile image
-  static constexpr int BYTES = 2 * IMG;                   // double-buffered
-  static constexpr int CPS = H * RB / 1024;    // 1 KiB DMA pieces per slice (4 rows each)
-  static constexpr int NCHW = CPS * L / W;     // DMA pieces per wave per tile
-  static_assert((H * RB) % 1024 == 0 && NCHW * W == CPS * L, "slice must be whole 1 KiB DMA pieces");
+  static constexpr int NBUF = NB ? NB : (2 * IMG <= 160 * 1024 ? 2 : 1);  // images (tiles in flight)
+  static constexpr int BYTES = NBUF * IMG;
+  static constexpr int RPP = 1024 / RB;        // peer rows per 1 KiB DMA piece
+  static constexpr int LPR = RB / 16;          // lanes per row of a piece
+  static constexpr int CPS = H * RB / 1024;    // pieces per slice
+  static constexpr int NCHW = CPS * L / W;     // pieces per loader wave per tile
+  static_assert(RB <= 1024 && (H * RB) % 1024 == 0 && NCHW * W == CPS * L, "whole 1 KiB DMA pieces");
+  static_assert(BYTES <= 160 * 1024, "LDS");
 };
 
 __device__ __forceinline__ void glds16(const float* src, uint8_t P2P_LDS* dst) {
@@ -260,25 +264,26 @@ __device__ __forceinline__ void block_sync_lds() {
   asm volatile("" ::: "memory");
 }
 
-// Block = L sorter waves + L loader waves.  Loaders only issue the LDS-DMA
+// Block = 4 sorter waves + 4 loader waves.  Loaders only issue the LDS-DMA
 // (a global_load_lds costs its wave ~100 cycles of issue; the sorters' VALU
 // stream never pays it); sorters read the image, sort, store.  The block
 // walks tiles t, t+grid, ... with two images: loaders keep the DMA of the
 // next tile in flight while the sorters work on the current one.  Per tile:
 //   loaders: wait own pieces of tile t | barrier A | barrier B | DMA(t+2 grid)
 //   sorters: (fill if not DMA-able)   | barrier A | read      | barrier B | sort, store
-template <int L, int H, int RULE, int MODE, bool SEGS>
-__global__ __launch_bounds__(128 * L) void robust_lds_kernel(const float* const* __restrict__ peers,
+template <int L, int H, int RULE, int MODE, bool SEGS, int NB>
+__global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __restrict__ peers,
                                                              const Seg* __restrict__ segs, int nseg,
                                                              int64_t ntiles, int K, int trim_b, int64_t n,
                                                              float* w, float* out, float lr) {
-  using Lay = LdsLayout<L, H>;
+  using Lay = LdsLayout<L, H, NB>;
+  static_assert(128 * Lay::W == 512, "launch bounds");
   __shared__ __attribute__((aligned(16))) uint8_t lds_raw[Lay::BYTES];
   uint8_t P2P_LDS* lds = (uint8_t P2P_LDS*)lds_raw;
   const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
-  const bool loader = wi >= L;  // wave-uniform role
-  const int li = wi - L;        // loader index
+  const bool loader = wi >= Lay::W;  // wave-uniform role
+  const int li = wi - Lay::W;        // loader index
   const int q = lane % L, c = wi * Lay::TW + lane / L;  // sorters: coordinate inside the block tile
 
   const int64_t nb = gridDim.x;
@@ -286,27 +291,35 @@ __global__ __launch_bounds__(128 * L) void robust_lds_kernel(const float* const*
   if ((nb & 7) == 0) t = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);  // XCD-contiguous tiles
   if (t >= ntiles) return;
 
-  // loaders: per-lane row pointers of their DMA pieces for the bound source
-  const float* rp[Lay::NCHW];
+  // loaders: per-lane row pointers of their DMA pieces for the bound source.
+  // Cached in VGPRs when two images are in flight (the loader must not wait
+  // on a pointer load while the next tile's DMA is outstanding); with one
+  // image they are reloaded per tile (L2 hits) so the sorters' 128 keys keep
+  // the register file.
+  constexpr bool kCachePtr = Lay::NBUF == 2;
+  const float* rp[kCachePtr ? Lay::NCHW : 1];
   int64_t cur_seg = -1;
   bool aligned = false;
+  auto row_of = [&](int m) {
+    const int ch = li * Lay::NCHW + m;
+    const int row = (ch / Lay::CPS) * H + (ch % Lay::CPS) * Lay::RPP + lane / Lay::LPR;
+    return row < K ? row : K - 1;
+  };
   auto bind = [&](const TileSrc& s) {
     if (s.seg == cur_seg) return;
     cur_seg = s.seg;
     aligned = all_aligned16(s.peers, K, s.w, nullptr);
-    if (loader) {
+    if constexpr (kCachePtr) {
+      if (loader) {
 #pragma unroll
-      for (int m = 0; m < Lay::NCHW; ++m) {
-        const int ch = li * Lay::NCHW + m;
-        const int row = (ch / Lay::CPS) * H + (ch % Lay::CPS) * 4 + lane / 16;
-        rp[m] = table_at(s.peers, row < K ? row : K - 1);
+        for (int m = 0; m < Lay::NCHW; ++m) rp[m] = table_at(s.peers, row_of(m));
       }
     }
   };
   auto dma_ok = [&](const TileSrc& s) { return aligned && s.c0 + Lay::TB <= s.n; };
   auto real_piece = [&](int m) {  // pieces made only of pad rows are skipped (MODE 0)
     const int ch = li * Lay::NCHW + m;
-    return MODE != 0 || (ch / Lay::CPS) * H + (ch % Lay::CPS) * 4 < K;
+    return MODE != 0 || (ch / Lay::CPS) * H + (ch % Lay::CPS) * Lay::RPP < K;
   };
   auto npieces = [&](const TileSrc& s) {
     int np = 0;
@@ -317,83 +330,102 @@ __global__ __launch_bounds__(128 * L) void robust_lds_kernel(const float* const*
   auto issue = [&](const TileSrc& s, int img_off) {
     if constexpr (P2P_LDS_DIAG == 1) return;
     uint8_t P2P_LDS* im = lds + img_off;
-    const int64_t off = s.c0 + 4 * (lane % 16);
+    const int64_t off = s.c0 + 4 * (lane % Lay::LPR);
 #pragma unroll
     for (int m = 0; m < Lay::NCHW; ++m) {
       const int ch = li * Lay::NCHW + m;
-      if (real_piece(m)) glds16(rp[m] + off, im + (ch / Lay::CPS) * Lay::SB + (ch % Lay::CPS) * 1024);
+      if (real_piece(m)) {
+        const float* src = kCachePtr ? rp[kCachePtr ? m : 0] : table_at(s.peers, row_of(m));
+        glds16(src + off, im + (ch / Lay::CPS) * Lay::SB + (ch % Lay::CPS) * 1024);
+      }
     }
-    if (s.w && li == 0 && lane < 16) glds16(s.w + s.c0 + 4 * lane, im + Lay::WOFF);
+    if (s.w && li == 0 && lane < Lay::LPR) glds16(s.w + s.c0 + 4 * lane, im + Lay::WOFF);
   };
 
+  // NBUF images: tile t in image `img` while the DMA of the next NBUF-1 tiles
+  // fills the others; the DMA of tile t + NBUF*grid goes into `img` as soon
+  // as tile t has been read into registers.  Loaders and sorters run separate
+  // loops (same tile sequence, same two barriers per tile) so neither role's
+  // registers are live across the other's code.
+  constexpr int D = Lay::NBUF;
   TileSrc cur = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t);
   bind(cur);
   bool dma_cur = dma_ok(cur);
   if (loader && dma_cur) issue(cur, 0);
   TileSrc nx1 = cur;
   bool dma_nx1 = false;
-  if (t + nb < ntiles) {
+  if (D == 2 && t + nb < ntiles) {
     nx1 = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t + nb);
     bind(nx1);
     dma_nx1 = dma_ok(nx1);
     if (loader && dma_nx1) issue(nx1, Lay::IMG);
   }
   int img = 0;
+  // the tile D grids ahead of t: located, and DMA'd by the loaders
+  auto advance = [&](int64_t tt) {
+    TileSrc nxd = D == 2 ? nx1 : cur;
+    bool dma_nxd = false;
+    if (tt + D * nb < ntiles) {
+      nxd = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, tt + D * nb);
+      bind(nxd);
+      dma_nxd = dma_ok(nxd);
+      if (loader && dma_nxd) issue(nxd, img);
+    }
+    if constexpr (D == 2) {
+      cur = nx1;
+      dma_cur = dma_nx1;
+      nx1 = nxd;
+      dma_nx1 = dma_nxd;
+      img ^= Lay::IMG;
+    } else {
+      cur = nxd;
+      dma_cur = dma_nxd;
+    }
+  };
 
+  if (loader) {
+    for (; t < ntiles; t += nb) {
+      block_sync_vm(D == 2 && dma_nx1 ? npieces(nx1) : 0);  // A: this loader's pieces of tile t landed
+      __builtin_amdgcn_s_barrier();                         // B: sorters have read the image
+      asm volatile("" ::: "memory");
+      advance(t);
+    }
+    return;
+  }
   for (; t < ntiles; t += nb) {
     uint8_t P2P_LDS* im = lds + img;
-    const int64_t i = cur.c0 + c;
+    const TileSrc me = cur;
+    const int64_t i = me.c0 + c;
+    if (!dma_cur) fill_direct<L, H>(im, me.peers, me.w, me.n, i, K, q, c);
+    __builtin_amdgcn_s_barrier();  // A: every piece of tile t is in the image
+    asm volatile("" ::: "memory");
     uint32_t v[H];
-    float wv = 0.f;
-    if (loader) {
-      block_sync_vm(dma_nx1 ? npieces(nx1) : 0);  // A: this loader's pieces of tile t landed
-      __builtin_amdgcn_s_barrier();               // B: sorters have read the image
-      asm volatile("" ::: "memory");
+    const uint32_t P2P_LDS* sl = (const uint32_t P2P_LDS*)(im + q * Lay::SB) + c;
+#pragma unroll
+    for (int j = 0; j < H; ++j) v[j] = sl[j * (Lay::RB / 4)];
+    const float wv = me.w ? ((const float P2P_LDS*)(im + Lay::WOFF))[c] : 0.f;
+    block_sync_lds();  // B: image consumed, free for the DMA D tiles ahead
+    advance(t);
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const bool real = (MODE != 0) || (q * H + j < K);
+      v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pads sort after every real key
+    }
+    bool own = false;
+    float agg;
+    if constexpr (P2P_LDS_DIAG == 2) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int j = 0; j < H; ++j) x ^= v[j];
+      agg = __uint_as_float(x);
+      own = q == 0;
     } else {
-      if (!dma_cur) fill_direct<L, H>(im, cur.peers, cur.w, cur.n, i, K, q, c);
-      __builtin_amdgcn_s_barrier();  // A: every piece of tile t is in the image
-      asm volatile("" ::: "memory");
-      const uint32_t P2P_LDS* sl = (const uint32_t P2P_LDS*)(im + q * Lay::SB) + c;
-#pragma unroll
-      for (int j = 0; j < H; ++j) v[j] = sl[j * (Lay::RB / 4)];
-      if (cur.w) wv = ((const float P2P_LDS*)(im + Lay::WOFF))[c];
-      block_sync_lds();  // B: image consumed, free for the DMA two tiles ahead
+      agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
     }
-    TileSrc nx2 = nx1;
-    bool dma_nx2 = false;
-    if (t + 2 * nb < ntiles) {
-      nx2 = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t + 2 * nb);
-      bind(nx2);
-      dma_nx2 = dma_ok(nx2);
-      if (loader && dma_nx2) issue(nx2, img);
+    if (own && i < me.n) {
+      if (me.out) stg(me.out + i, agg);
+      if (me.w) stg(me.w + i, apply_lr(wv, lr, agg));
     }
-    if (!loader) {
-#pragma unroll
-      for (int j = 0; j < H; ++j) {
-        const bool real = (MODE != 0) || (q * H + j < K);
-        v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pads sort after every real key
-      }
-      bool own = false;
-      float agg;
-      if constexpr (P2P_LDS_DIAG == 2) {
-        uint32_t x = 0;
-#pragma unroll
-        for (int j = 0; j < H; ++j) x ^= v[j];
-        agg = __uint_as_float(x);
-        own = q == 0;
-      } else {
-        agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
-      }
-      if (own && i < cur.n) {
-        if (cur.out) stg(cur.out + i, agg);
-        if (cur.w) stg(cur.w + i, apply_lr(wv, lr, agg));
-      }
-    }
-    cur = nx1;
-    dma_cur = dma_nx1;
-    nx1 = nx2;
-    dma_nx1 = dma_nx2;
-    img ^= Lay::IMG;
   }
 }
 
@@ -410,39 +442,39 @@ struct LdsArgs {
   hipStream_t stream;
 };
 
-template <int L, int H, int RULE, int MODE, bool SEGS>
+template <int L, int H, int RULE, int MODE, bool SEGS, int NB>
 static void launch_lds_kernel(const LdsArgs& a) {
-  using Lay = LdsLayout<L, H>;
-  auto kern = robust_lds_kernel<L, H, RULE, MODE, SEGS>;
+  using Lay = LdsLayout<L, H, NB>;
+  auto kern = robust_lds_kernel<L, H, RULE, MODE, SEGS, NB>;
   static int resident = 0;  // persistent grid: every resident block slot once
   if (resident == 0) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 128 * L, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 128 * Lay::W, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int64_t ntiles = SEGS ? a.tiles : ceil_div(a.n, Lay::TB);
   const int64_t grid = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(128 * L), 0, a.stream, a.peers, a.segs, a.nseg,
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(128 * Lay::W), 0, a.stream, a.peers, a.segs, a.nseg,
                      ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
 }
 
-template <int L, int H, int RULE, int MODE>
+template <int L, int H, int RULE, int MODE, int NB>
 static void launch_lds_mode(const LdsArgs& a) {
-  if (a.segs) launch_lds_kernel<L, H, RULE, MODE, true>(a);
-  else launch_lds_kernel<L, H, RULE, MODE, false>(a);
+  if (a.segs) launch_lds_kernel<L, H, RULE, MODE, true, NB>(a);
+  else launch_lds_kernel<L, H, RULE, MODE, false, NB>(a);
 }
 
-template <int L, int H, int RULE>
+template <int L, int H, int RULE, int NB = 0>
 static void launch_lds(const LdsArgs& a) {
   constexpr int KP = L * H;
   if constexpr (RULE == P2P_RULE_MEDIAN) {
-    if (a.K == KP) return launch_lds_mode<L, H, RULE, 1>(a);
+    if (a.K == KP) return launch_lds_mode<L, H, RULE, 1, NB>(a);
   } else {
-    if (a.K == KP && a.trim_b == (KP * 2) / 10) return launch_lds_mode<L, H, RULE, 2>(a);
+    if (a.K == KP && a.trim_b == (KP * 2) / 10) return launch_lds_mode<L, H, RULE, 2, NB>(a);
   }
-  launch_lds_mode<L, H, RULE, 0>(a);
+  launch_lds_mode<L, H, RULE, 0, NB>(a);
 }
 
 }  // namespace p2p
@@ -450,10 +482,11 @@ static void launch_lds(const LdsArgs& a) {
 using namespace p2p;
 
 // Layout for K (p2p_robust_lds_tile and the launch must agree): K in 129..256
-// -> 4 lanes x 64 keys; K in 65..128 -> 4 lanes x 32 keys, or 2 lanes x 64
-// keys when variant == 1 (tuning knob, see robust.hip).
+// -> 4 lanes x 64 keys; K in 65..128 -> 4 lanes x 32 keys (variant 0), 2
+// lanes x 64 keys (1) or one lane x 128 keys (2) (tuning knob, robust.hip).
 extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t k, int32_t variant) {
-  return 64;  // every layout: 64-coordinate block tiles
+  if (k > 128) return LdsLayout<4, 64>::TB;
+  return variant == 1 ? LdsLayout<2, 64>::TB : variant == 2 ? LdsLayout<1, 128>::TB : LdsLayout<4, 32>::TB;
 }
 
 extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, const p2p_segment_t* segs,
@@ -466,6 +499,8 @@ extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, co
     if (med) launch_lds<4, 64, P2P_RULE_MEDIAN>(a); else launch_lds<4, 64, P2P_RULE_TRIMMED>(a);
   } else if (variant == 1) {
     if (med) launch_lds<2, 64, P2P_RULE_MEDIAN>(a); else launch_lds<2, 64, P2P_RULE_TRIMMED>(a);
+  } else if (variant == 2) {
+    if (med) launch_lds<1, 128, P2P_RULE_MEDIAN>(a); else launch_lds<1, 128, P2P_RULE_TRIMMED>(a);
   } else {
     if (med) launch_lds<4, 32, P2P_RULE_MEDIAN>(a); else launch_lds<4, 32, P2P_RULE_TRIMMED>(a);
   }

@@ -16,7 +16,7 @@ except Exception: print(l[-600:])"; return $rc; }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
   run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread || exit $?
 fi
-for impl in ${IMPLS:-auto lds lds2 group}; do
+for impl in ${IMPLS:-auto lds lds2 lds1 group}; do
   for wl in ${WLS:-median256 trimmed256 cfg4-median cfg4-trimmed}; do
     run "${wl}_$impl" 300 env P2P_ROBUST_IMPL=$impl python bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline || exit $?
   done

@@ -39,9 +39,10 @@ def test_abi_version_and_argument_errors_without_gpu():
     assert L.p2p_tile_elems(1, 128) == 128 and L.p2p_tile_elems(1, 200) == 64 and L.p2p_tile_elems(2, 129) == 64
     try:  # layout knob: LDS-staged kernels for K <= 128 too, and the legacy kernels
         assert L.p2p_set_robust_layout(1) == 0 and L.p2p_tile_elems(1, 128) == 64 and L.p2p_tile_elems(1, 64) == 128
-        assert L.p2p_set_robust_layout(2) == 0 and L.p2p_tile_elems(1, 100) == 64
+        assert L.p2p_set_robust_layout(2) == 0 and L.p2p_tile_elems(1, 100) == 128
         assert L.p2p_set_robust_layout(3) == 0 and L.p2p_tile_elems(1, 128) == 128 and L.p2p_tile_elems(1, 200) == 64
-        assert L.p2p_set_robust_layout(4) == -1
+        assert L.p2p_set_robust_layout(4) == 0 and L.p2p_tile_elems(1, 128) == 256 and L.p2p_tile_elems(1, 200) == 64
+        assert L.p2p_set_robust_layout(5) == -1
     finally:
         L.p2p_set_robust_layout(0)
     # argument validation happens before any HIP call
