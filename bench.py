@@ -233,6 +233,13 @@ def run_delta_workload(args, n, seed, dev):
     step_s = (time.perf_counter() - t0) / args.steps
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     alg = 16 * n
+    traffic = None
+    tfile = os.path.join(REPO, "profiles", "traffic_delta.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tj = json.load(f)
+        if tj.get("coords_per_launch") == n:
+            traffic = tj.get("hbm_bytes_per_launch")
     cpu = None
     if not args.no_cpu_baseline:
         import oracle.cpu_baseline as cb  # baseline leg only
@@ -252,8 +259,8 @@ def run_delta_workload(args, n, seed, dev):
         "config": {"workload": f"delta: trainer local update over {n:,} fp32 params (SURVEY §8(f) row 2)",
                    "coords_per_gpu": n, "parallelism": "single GPU (replicas only)"},
         "roofline": {"bound": "hbm", "achieved": round(alg / (kern_ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(alg / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg},
+                     "unit": "GB/s", "frac": round(alg / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg},
         "cpu_baseline": cpu}), flush=True)
 
 

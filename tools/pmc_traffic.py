@@ -45,8 +45,10 @@ def main():
     wv, write_kib = per_dispatch(wdir, "WRITE_SIZE", kname)
     read_b = 2 * fetch_kib * 1024  # gfx950 half-count of wide streaming reads
     write_b = write_kib * 1024
-    alg_read = 4 * coords * (peers + 1)
-    alg_write = 4 * coords
+    if workload == "delta":  # read cur + prev, write delta + prev (16 B per parameter)
+        alg_read, alg_write = 8 * coords, 8 * coords
+    else:  # K peer reads + w read, w write
+        alg_read, alg_write = 4 * coords * (peers + 1), 4 * coords
     res = {
         "workload": workload, "kernel": kname, "coords_per_launch": coords, "peers": peers,
         "dispatches": [len(fv), len(wv)],
