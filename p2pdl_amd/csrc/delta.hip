@@ -26,30 +26,39 @@ __device__ __forceinline__ void st4_nt(float* p, f4 v) {
   __builtin_nontemporal_store(v, (P2P_GLOBAL f4*)(p));
 }
 
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, f4 v) {
+  if (NT) st4_nt(p, v); else *reinterpret_cast<f4*>(p) = v;
+}
+
+// One tile of kBlock*4*NV floats (the segments kernel and the ABI's
+// P2P_DELTA_TILE use NV = kDNV).
+template <int NV = kDNV, bool NT = true>
 __device__ __forceinline__ void delta_tile(const float* cur, float* prev, float* delta, int64_t n,
                                            int64_t tile0, bool first) {
+  constexpr int kT = kBlock * 4 * NV;
   const int64_t base = tile0 + 4 * static_cast<int64_t>(threadIdx.x);
   const bool aligned =
       ((reinterpret_cast<uintptr_t>(cur) | reinterpret_cast<uintptr_t>(prev) | reinterpret_cast<uintptr_t>(delta)) &
        15) == 0;
-  if (aligned && tile0 + kDTile <= n) {
-    f4 c[kDNV], p[kDNV];
+  if (aligned && tile0 + kT <= n) {
+    f4 c[NV], p[NV];
 #pragma unroll
-    for (int v = 0; v < kDNV; ++v) c[v] = ld4_nt(cur + base + kBlock * 4 * v);
+    for (int v = 0; v < NV; ++v) c[v] = ld4_nt(cur + base + kBlock * 4 * v);
     if (!first) {
 #pragma unroll
-      for (int v = 0; v < kDNV; ++v) p[v] = ld4_nt(prev + base + kBlock * 4 * v);
+      for (int v = 0; v < NV; ++v) p[v] = ld4_nt(prev + base + kBlock * 4 * v);
     }
 #pragma unroll
-    for (int v = 0; v < kDNV; ++v) {
+    for (int v = 0; v < NV; ++v) {
       const int64_t o = base + kBlock * 4 * v;
-      st4_nt(delta + o, first ? c[v] : c[v] - p[v]);  // (:279) or the first-round copy (:275)
-      st4_nt(prev + o, c[v]);                          // clone (:282)
+      st4<NT>(delta + o, first ? c[v] : c[v] - p[v]);  // (:279) or the first-round copy (:275)
+      st4<NT>(prev + o, c[v]);                          // clone (:282)
     }
     return;
   }
 #pragma unroll 1
-  for (int v = 0; v < kDNV; ++v)
+  for (int v = 0; v < NV; ++v)
 #pragma unroll 1
     for (int e = 0; e < 4; ++e) {
       const int64_t i = base + kBlock * 4 * v + e;
@@ -60,9 +69,10 @@ __device__ __forceinline__ void delta_tile(const float* cur, float* prev, float*
     }
 }
 
+template <int NV, bool NT>
 __global__ __launch_bounds__(kBlock) void delta_flat_kernel(const float* cur, float* prev, float* delta,
                                                             int64_t n, int first) {
-  delta_tile(cur, prev, delta, n, static_cast<int64_t>(blockIdx.x) * kDTile, first != 0);
+  delta_tile<NV, NT>(cur, prev, delta, n, static_cast<int64_t>(blockIdx.x) * (kBlock * 4 * NV), first != 0);
 }
 
 // Whole state_dict: one tile per block, segment by binary search on tile_begin.
@@ -83,7 +93,7 @@ __global__ __launch_bounds__(kBlock) void delta_segments_kernel(const p2p_delta_
   float* delta = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->delta))));
   const int64_t n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
   const int64_t tb = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->tile_begin))));
-  delta_tile(cur, prev, delta, n, (t - tb) * kDTile, first != 0);
+  delta_tile<kDNV, true>(cur, prev, delta, n, (t - tb) * kDTile, first != 0);
 }
 
 }  // namespace p2p
@@ -102,10 +112,31 @@ extern "C" int32_t p2p_delta_snapshot_f32(const float* cur, float* prev, float* 
       3)
     return P2P_ERR_ALIGN;
   if (n == 0) return P2P_OK;
-  const int64_t tiles = ceil_div(n, kDTile);
+  // Tuning knobs (measured in DESIGN.md): floats per lane per tensor (NV x 4)
+  // and nontemporal vs plain stores.
+  static const int nv = [] {
+    const char* e = getenv("P2P_DELTA_NV");
+    const int v = e ? atoi(e) : kDNV;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : kDNV;
+  }();
+  static const bool nt = [] {
+    const char* e = getenv("P2P_DELTA_NT");
+    return !(e && atoi(e) == 0);
+  }();
+  const int64_t tiles = ceil_div(n, static_cast<int64_t>(kBlock) * 4 * nv);
+  hipStream_t s = static_cast<hipStream_t>(stream);
   if (tiles > 0x7FFFFFFFll) return P2P_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(delta_flat_kernel, dim3(static_cast<unsigned>(tiles)), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), cur, prev, delta, n, first);
+  const dim3 g(static_cast<unsigned>(tiles)), b(kBlock);
+#define P2P_DLAUNCH(NV_)                                                                              \
+  if (nt) hipLaunchKernelGGL((delta_flat_kernel<NV_, true>), g, b, 0, s, cur, prev, delta, n, first); \
+  else hipLaunchKernelGGL((delta_flat_kernel<NV_, false>), g, b, 0, s, cur, prev, delta, n, first)
+  switch (nv) {
+    case 1: P2P_DLAUNCH(1); break;
+    case 2: P2P_DLAUNCH(2); break;
+    case 8: P2P_DLAUNCH(8); break;
+    default: P2P_DLAUNCH(4); break;
+  }
+#undef P2P_DLAUNCH
   return delta_status();
 }
 
