@@ -65,6 +65,16 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, int reps) {
         asm volatile(OPB("v_add_u32") OPB("v_add_u32") OPB("v_add_u32") OPB("v_add_u32") ::: "v8", "v9", "v10", "v11", "v12", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
       else if constexpr (MODE == 10)
         asm volatile(OP3("v_bitop3_b32") OP3("v_bitop3_b32") OP3("v_bitop3_b32") OP3("v_bitop3_b32") ::: "v8", "v9", "v10", "v11", "v12", "v13", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
+      // packed 16-bit compare-exchange halves (two 16-bit keys per VGPR): the
+      // candidate for a two-pass hi16 / lo16 radix median
+      else if constexpr (MODE == 12)
+        asm volatile(OPB("v_pk_min_u16") OPB("v_pk_max_u16") OPB("v_pk_min_u16") OPB("v_pk_max_u16") ::: "v8", "v9", "v10", "v11", "v12", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
+      else if constexpr (MODE == 13)
+        asm volatile(OPB("v_min_u16") OPB("v_max_u16") OPB("v_min_u16") OPB("v_max_u16") ::: "v8", "v9", "v10", "v11", "v12", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
+      else if constexpr (MODE == 14)
+        asm volatile(OPB("v_pk_add_u16") OPB("v_pk_add_u16") OPB("v_pk_add_u16") OPB("v_pk_add_u16") ::: "v8", "v9", "v10", "v11", "v12", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
+      else if constexpr (MODE == 15)
+        asm volatile(OPB("v_pk_min_f16") OPB("v_pk_max_f16") OPB("v_pk_min_f16") OPB("v_pk_max_f16") ::: "v8", "v9", "v10", "v11", "v12", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
       else
         asm volatile(OPD OPD OPD OPD ::: "v8", "v9", "v10", "v11", "v12", "v13", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47");
     } else {  // different-bank pairs only: v8 vs v9, ...
@@ -120,6 +130,10 @@ int main() {
     run<10>("v_bitop3_b32", out, w);
     run<8>("v_cmp(e64)+cndmask mix", out, w);
     run<11>("v_mov_b32_dpp", out, w);
+    run<12>("v_pk_min/max_u16", out, w);
+    run<13>("v_min/max_u16", out, w);
+    run<14>("v_pk_add_u16", out, w);
+    run<15>("v_pk_min/max_f16", out, w);
   }
   return 0;
 }
