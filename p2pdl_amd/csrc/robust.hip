@@ -444,6 +444,8 @@ extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, co
 //   2 "lds2"   robust_lds.hip, 2 lanes x 64 keys at K <= 128
 //   3 "group"  this file only: one lane (K <= 128) / 4-wave LDS group (K > 128)
 //   4 "lds1"   robust_lds.hip, one lane x 128 keys (LDS-DMA staged) at K <= 128
+//   5 "radix16" as auto, except median at K = 256: two-pass radix median with
+//              packed 16-bit hi-half networks (robust_lds.hip, 128-coord tiles)
 // (Measured and dropped: one LDS image per block with two blocks per CU for
 // K > 128 -- 2 sorter waves per SIMD -- ran the same 26.6 ms as one block
 // with two images: the K = 256 kernel is VALU-bound)
@@ -454,20 +456,22 @@ static int robust_impl() {
     int v = 0;
     if (e && e[0] == 'g') v = 3;
     else if (e && e[0] == 'l' && e[1] == 'd' && e[2] == 's') v = (e[3] == '2') ? 2 : (e[3] == '1') ? 4 : 1;
+    else if (e && e[0] == 'r') v = 5;
     g_robust_impl = v;
   }
   return g_robust_impl;
 }
 
-// Which robust_lds.hip variant serves (k, impl), or -1 for this file's kernels.
-static int lds_variant(int k, int impl) {
+// Which robust_lds.hip variant serves (rule, k, impl), or -1 for this file's kernels.
+static int lds_variant(int rule, int k, int impl) {
+  if (impl == 5 && k == 256 && rule == P2P_RULE_MEDIAN) return 3;
   if (k <= 64 || impl == 3) return -1;
   if (k > 128) return 0;
   return impl == 1 ? 0 : impl == 2 ? 1 : impl == 4 ? 2 : -1;
 }
 
 extern "C" int32_t p2p_set_robust_layout(int32_t layout) {
-  if (layout < 0 || layout > 4) return P2P_ERR_INVALID;
+  if (layout < 0 || layout > 5) return P2P_ERR_INVALID;
   g_robust_impl = layout;
   return P2P_OK;
 }
@@ -480,7 +484,7 @@ extern "C" P2P_INTERNAL int32_t p2p_robust_dispatch(const float* const* peers, c
   if (k > 256) return P2P_ERR_UNSUPPORTED;
   if (rule == P2P_RULE_TRIMMED && (trim_b < 0 || k - 2 * trim_b <= 0)) return P2P_ERR_INVALID;
   if (rule != P2P_RULE_MEDIAN && rule != P2P_RULE_TRIMMED) return P2P_ERR_INVALID;
-  const int var = lds_variant(k, robust_impl());
+  const int var = lds_variant(rule, k, robust_impl());
   if (var >= 0) {
     p2p_robust_lds_launch(peers, segs, nseg, tiles, k, rule, trim_b, n, w, out, lr, var, stream);
   } else {
@@ -492,8 +496,7 @@ extern "C" P2P_INTERNAL int32_t p2p_robust_dispatch(const float* const* peers, c
 }
 
 extern "C" P2P_INTERNAL int64_t p2p_robust_tile_elems(int32_t rule, int32_t k) {
-  (void)rule;
-  const int var = lds_variant(k, robust_impl());
+  const int var = lds_variant(rule, k, robust_impl());
   if (var >= 0) return p2p_robust_lds_tile(k, var);
   return k > 128 ? kGroupTile : kRobustTile;
 }

@@ -36,6 +36,15 @@
 // Tiles that cannot be DMA'd (a peer / w pointer not 16-B aligned, or the
 // ragged last tile of a buffer) load the same keys with per-lane global
 // loads; the arithmetic after the load is the same code.
+// Packed 16-bit keys (two coordinates per VGPR, radix16 layout): declared
+// before the networks so their unqualified min / max calls resolve for u16x2.
+#include <hip/hip_runtime.h>
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 min(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ u16x2 max(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ u16x2 pmin(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ u16x2 pmax(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
+
 #include "robust_nets.h"
 
 #define P2P_LDS __attribute__((address_space(3)))
@@ -71,11 +80,11 @@ __device__ __forceinline__ float from_prev_slice(float x) {
   return __uint_as_float(dpp<L == 4 ? 0x90 : 0xA0>(__float_as_uint(x)));
 }
 
-template <int L, int H, int NB = 0>
+template <int L, int H, int NB = 0, int PK = 1>
 struct LdsLayout {
   static constexpr int W = 4;                  // sorter waves per block (and as many loaders)
-  static constexpr int TB = 64 * W / L;        // coordinates per block tile
-  static constexpr int TW = 64 / L;            // coordinates per sorter wave
+  static constexpr int TB = 64 * W * PK / L;   // coordinates per block tile
+  static constexpr int TW = 64 * PK / L;       // coordinates per sorter wave (PK per lane group)
   static constexpr int RB = 4 * TB;            // bytes per peer row (>= 256 contiguous in HBM)
   static constexpr int PAD = L > 1 ? 128 / L : 0;
   static constexpr int SB = H * RB + PAD;      // bytes per slice
@@ -215,15 +224,93 @@ __device__ __forceinline__ float reduce_keys(uint32_t (&v)[H], int q, int K, int
   }
 }
 
+// ---- two-pass radix median, K = 256 (layout "radix16", PK = 2) -------------
+// Two coordinates per lane group: lane 4c+q holds keys 64q..64q+63 of
+// coordinates c (ka) and c+16 (kb).  Pass 1 runs the L = 4 median chain on
+// packed u16x2 keys -- the hi16 halves of both coordinates in one VGPR --
+// because v_pk_min/max_u16 sort two keys per half-rate instruction
+// (profiles/r01/probes: 0.61x the VALU time per coordinate of the uint32
+// chain).  It yields mh = hi16 of the rank-127 key and the rank-126 hi16.
+// When rank 126's hi16 < mh, exactly 127 keys lie below mh's bucket, so the
+// median is the SMALLEST key whose hi16 is mh: one min over (key - mh<<16)
+// (keys below the bucket wrap above 2^16, keys above it are >= 2^16).
+// Otherwise (a tie of hi16 across ranks 126/127 anywhere in the wave) the
+// wave runs the exact uint32 chain on both coordinates.
+__device__ __forceinline__ uint32_t pbits(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ u16x2 pvec(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+template <int M>
+__device__ __forceinline__ u16x2 pxq(u16x2 x) { return pvec(xq<M>(pbits(x))); }
+__device__ __forceinline__ u16x2 pkeep(u16x2 a, u16x2 pa, bool hi) {
+  const u16x2 lo = pmin(a, pa), h = pmax(a, pa);
+  return hi ? h : lo;
+}
+
+__device__ __forceinline__ void radix_median_pair(uint32_t (&ka)[64], uint32_t (&kb)[64], int q, float& ra,
+                                                  float& rb) {
+  u16x2 h[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) h[j] = pvec((ka[j] >> 16) | (kb[j] & 0xFFFF0000u));
+  sort_full<64>(h);  // the generated networks are type-generic (min / max below)
+  const bool k1 = q & 1, k2 = q & 2;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {  // flip against lane q^1
+    const u16x2 a = h[j], b = h[63 - j];
+    h[j] = pkeep(a, pxq<1>(b), k1);
+    h[63 - j] = pkeep(b, pxq<1>(a), k1);
+  }
+  bmerge<64>(h);
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {  // flip against lane q^3
+    const u16x2 a = h[j], b = h[63 - j];
+    h[j] = pkeep(a, pxq<3>(b), k2);
+    h[63 - j] = pkeep(b, pxq<3>(a), k2);
+  }
+  // lanes q < 2 now hold the 128 smallest hi16 of each coordinate: the
+  // largest two of them are ranks 127 and 126
+  u16x2 m1 = h[0], m2 = pvec(0u);
+#pragma unroll
+  for (int j = 1; j < 64; ++j) {
+    m2 = pmax(m2, pmin(m1, h[j]));
+    m1 = pmax(m1, h[j]);
+  }
+  {
+    const u16x2 p1 = pxq<1>(m1), p2 = pxq<1>(m2);
+    m2 = pmax(pmin(m1, p1), pmax(m2, p2));
+    m1 = pmax(m1, p1);
+  }
+  const uint32_t mh = dpp<0x00>(pbits(m1)), sh = dpp<0x00>(pbits(m2));  // lane 4c's values to its quad
+  const uint32_t mha = mh & 0xFFFFu, mhb = mh >> 16;
+  const bool fast = (sh & 0xFFFFu) < mha && (sh >> 16) < mhb;
+  if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
+    const uint32_t ba = mha << 16, bb = mhb << 16;
+    uint32_t ua = 0xFFFFFFFFu, ub = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      ua = min(ua, ka[j] - ba);
+      ub = min(ub, kb[j] - bb);
+    }
+    ua = min(ua, xq<1>(ua));
+    ub = min(ub, xq<1>(ub));
+    ua = min(ua, xq<2>(ua));
+    ub = min(ub, xq<2>(ub));
+    ra = __uint_as_float(key2f(ua + ba));
+    rb = __uint_as_float(key2f(ub + bb));
+  } else {  // valid in lane q == 0 either way
+    bool own = false;
+    ra = reduce_keys<4, 64, P2P_RULE_MEDIAN, 1>(ka, q, 256, 0, own);
+    rb = reduce_keys<4, 64, P2P_RULE_MEDIAN, 1>(kb, q, 256, 0, own);
+  }
+}
+
 // Register-staged fill of the LDS image for a tile that cannot be DMA'd
 // (misaligned pointer or ragged tail): each lane writes exactly the words it
 // reads back.  Out of line: its row-pointer loads must not share the
 // register budget of the sorting loop.
-template <int L, int H>
+template <int L, int H, int PK>
 __device__ __attribute__((noinline)) void fill_direct(uint8_t P2P_LDS* lds, const float* const* tbl,
                                                       const float* w, int64_t n, int64_t i, int K, int q,
                                                       int c) {
-  using Lay = LdsLayout<L, H>;
+  using Lay = LdsLayout<L, H, 0, PK>;
   const int64_t ic = i < n ? i : n - 1;  // dead lanes re-read the last element
   uint32_t P2P_LDS* sl = (uint32_t P2P_LDS*)(lds + q * Lay::SB) + c;
 #pragma unroll
@@ -271,13 +358,14 @@ __device__ __forceinline__ void block_sync_lds() {
 // next tile in flight while the sorters work on the current one.  Per tile:
 //   loaders: wait own pieces of tile t | barrier A | barrier B | DMA(t+2 grid)
 //   sorters: (fill if not DMA-able)   | barrier A | read      | barrier B | sort, store
-template <int L, int H, int RULE, int MODE, bool SEGS, int NB>
+template <int L, int H, int RULE, int MODE, bool SEGS, int NB, int PK = 1>
 __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __restrict__ peers,
                                                              const Seg* __restrict__ segs, int nseg,
                                                              int64_t ntiles, int K, int trim_b, int64_t n,
                                                              float* w, float* out, float lr) {
-  using Lay = LdsLayout<L, H, NB>;
+  using Lay = LdsLayout<L, H, NB, PK>;
   static_assert(128 * Lay::W == 512, "launch bounds");
+  static_assert(PK == 1 || (L == 4 && H == 64 && RULE == P2P_RULE_MEDIAN && MODE == 1), "radix16: median of 256");
   __shared__ __attribute__((aligned(16))) uint8_t lds_raw[Lay::BYTES];
   uint8_t P2P_LDS* lds = (uint8_t P2P_LDS*)lds_raw;
   const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -296,7 +384,7 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
   // on a pointer load while the next tile's DMA is outstanding); with one
   // image they are reloaded per tile (L2 hits) so the sorters' 128 keys keep
   // the register file.
-  constexpr bool kCachePtr = Lay::NBUF == 2;
+  constexpr bool kCachePtr = Lay::NBUF == 2 || PK == 2;  // radix16: one image, VGPRs to spare
   const float* rp[kCachePtr ? Lay::NCHW : 1];
   int64_t cur_seg = -1;
   bool aligned = false;
@@ -396,7 +484,10 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
     uint8_t P2P_LDS* im = lds + img;
     const TileSrc me = cur;
     const int64_t i = me.c0 + c;
-    if (!dma_cur) fill_direct<L, H>(im, me.peers, me.w, me.n, i, K, q, c);
+    if (!dma_cur) {
+      fill_direct<L, H, PK>(im, me.peers, me.w, me.n, i, K, q, c);
+      if constexpr (PK == 2) fill_direct<L, H, PK>(im, me.peers, me.w, me.n, i + 64 / L, K, q, c + 64 / L);
+    }
     __builtin_amdgcn_s_barrier();  // A: every piece of tile t is in the image
     asm volatile("" ::: "memory");
     uint32_t v[H];
@@ -404,6 +495,33 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
 #pragma unroll
     for (int j = 0; j < H; ++j) v[j] = sl[j * (Lay::RB / 4)];
     const float wv = me.w ? ((const float P2P_LDS*)(im + Lay::WOFF))[c] : 0.f;
+    if constexpr (PK == 2) {  // radix16: the lane group's second coordinate, c + 16
+      constexpr int C2 = 64 / L;
+      uint32_t v2[H];
+#pragma unroll
+      for (int j = 0; j < H; ++j) v2[j] = sl[j * (Lay::RB / 4) + C2];
+      const float wv2 = me.w ? ((const float P2P_LDS*)(im + Lay::WOFF))[c + C2] : 0.f;
+      block_sync_lds();  // B
+      advance(t);
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        v[j] = f2key(v[j]);
+        v2[j] = f2key(v2[j]);
+      }
+      float a1, a2;
+      radix_median_pair(v, v2, q, a1, a2);
+      if (q == 0) {
+        if (i < me.n) {
+          if (me.out) stg(me.out + i, a1);
+          if (me.w) stg(me.w + i, apply_lr(wv, lr, a1));
+        }
+        if (i + C2 < me.n) {
+          if (me.out) stg(me.out + i + C2, a2);
+          if (me.w) stg(me.w + i + C2, apply_lr(wv2, lr, a2));
+        }
+      }
+      continue;
+    }
     block_sync_lds();  // B: image consumed, free for the DMA D tiles ahead
     advance(t);
 #pragma unroll
@@ -442,10 +560,10 @@ struct LdsArgs {
   hipStream_t stream;
 };
 
-template <int L, int H, int RULE, int MODE, bool SEGS, int NB>
+template <int L, int H, int RULE, int MODE, bool SEGS, int NB, int PK = 1>
 static void launch_lds_kernel(const LdsArgs& a) {
-  using Lay = LdsLayout<L, H, NB>;
-  auto kern = robust_lds_kernel<L, H, RULE, MODE, SEGS, NB>;
+  using Lay = LdsLayout<L, H, NB, PK>;
+  auto kern = robust_lds_kernel<L, H, RULE, MODE, SEGS, NB, PK>;
   static int resident = 0;  // persistent grid: every resident block slot once
   if (resident == 0) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -485,6 +603,7 @@ using namespace p2p;
 // -> 4 lanes x 64 keys; K in 65..128 -> 4 lanes x 32 keys (variant 0), 2
 // lanes x 64 keys (1) or one lane x 128 keys (2) (tuning knob, robust.hip).
 extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t k, int32_t variant) {
+  if (variant == 3) return LdsLayout<4, 64, 0, 2>::TB;  // radix16 (median, K = 256 only)
   if (k > 128) return LdsLayout<4, 64>::TB;
   return variant == 1 ? LdsLayout<2, 64>::TB : variant == 2 ? LdsLayout<1, 128>::TB : LdsLayout<4, 32>::TB;
 }
@@ -495,7 +614,10 @@ extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, co
                                                    int32_t variant, p2p_stream_t stream) {
   LdsArgs a{peers, segs, nseg, tiles, k, trim_b, n, w, out, lr, static_cast<hipStream_t>(stream)};
   const bool med = rule == P2P_RULE_MEDIAN;
-  if (k > 128) {
+  if (variant == 3) {  // radix16: the caller routes only median at K = 256 here
+    if (segs) launch_lds_kernel<4, 64, P2P_RULE_MEDIAN, 1, true, 0, 2>(a);
+    else launch_lds_kernel<4, 64, P2P_RULE_MEDIAN, 1, false, 0, 2>(a);
+  } else if (k > 128) {
     if (med) launch_lds<4, 64, P2P_RULE_MEDIAN>(a); else launch_lds<4, 64, P2P_RULE_TRIMMED>(a);
   } else if (variant == 1) {
     if (med) launch_lds<2, 64, P2P_RULE_MEDIAN>(a); else launch_lds<2, 64, P2P_RULE_TRIMMED>(a);

@@ -321,7 +321,7 @@ def fill_synthetic_(out: torch.Tensor, seed: int, peer: int, scale: float, chunk
     return out
 
 
-ROBUST_LAYOUTS = {"auto": 0, "lds": 1, "lds2": 2, "group": 3, "lds1": 4}
+ROBUST_LAYOUTS = {"auto": 0, "lds": 1, "lds2": 2, "group": 3, "lds1": 4, "radix16": 5}
 
 
 def set_robust_layout(layout: str | int) -> None:

@@ -42,7 +42,10 @@ def test_abi_version_and_argument_errors_without_gpu():
         assert L.p2p_set_robust_layout(2) == 0 and L.p2p_tile_elems(1, 100) == 128
         assert L.p2p_set_robust_layout(3) == 0 and L.p2p_tile_elems(1, 128) == 128 and L.p2p_tile_elems(1, 200) == 64
         assert L.p2p_set_robust_layout(4) == 0 and L.p2p_tile_elems(1, 128) == 256 and L.p2p_tile_elems(1, 200) == 64
-        assert L.p2p_set_robust_layout(5) == -1
+        # radix16: 128-coordinate tiles for the median of exactly 256, else auto
+        assert L.p2p_set_robust_layout(5) == 0 and L.p2p_tile_elems(1, 256) == 128 and L.p2p_tile_elems(2, 256) == 64
+        assert L.p2p_tile_elems(1, 255) == 64 and L.p2p_tile_elems(1, 128) == 128
+        assert L.p2p_set_robust_layout(6) == -1
     finally:
         L.p2p_set_robust_layout(0)
     # argument validation happens before any HIP call

@@ -206,7 +206,7 @@ def test_robust_vs_oracle(cuda, rule, k):
     assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k}")
 
 
-@pytest.fixture(params=["auto", "lds", "lds2", "lds1", "group"])
+@pytest.fixture(params=["auto", "lds", "lds2", "lds1", "group", "radix16"])
 def robust_layout(request):
     ops.set_robust_layout(request.param)
     yield request.param
