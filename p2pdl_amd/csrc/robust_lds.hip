@@ -509,7 +509,18 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
         v2[j] = f2key(v2[j]);
       }
       float a1, a2;
-      radix_median_pair(v, v2, q, a1, a2);
+      if constexpr (P2P_LDS_DIAG == 2) {  // staging only
+        uint32_t x = 0, y = 0;
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+          x ^= v[j];
+          y ^= v2[j];
+        }
+        a1 = __uint_as_float(x);
+        a2 = __uint_as_float(y);
+      } else {
+        radix_median_pair(v, v2, q, a1, a2);
+      }
       if (q == 0) {
         if (i < me.n) {
           if (me.out) stg(me.out + i, a1);
