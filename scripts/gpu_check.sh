@@ -12,7 +12,7 @@ cd "$ROOT"
 run() { local name=$1 t=$2; shift 2; local s=$SECONDS
   timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
   echo "$name rc=$rc $((SECONDS-s))s"; tail -3 "$OUT/$name.log"; return $rc; }
-run pytest_gpu 900 python -m pytest tests -m gpu -q -rf; rc=$?
+run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread; rc=$?
 if [ $rc -gt 1 ]; then exit $rc; fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 for extra in "${@:2}"; do :; done
