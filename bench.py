@@ -2,20 +2,35 @@
 """Benchmark of the aggregation hot path (driver contract: one JSON line).
 
 Metric (BASELINE.json): aggregated peer-update GB/s (% HBM peak) at 1/2/4/8
-MI355X.  Default workload = cfg3's per-GPU coordinate tile: 256 peers x 125M
-fp32 coordinates PER GPU (weak scaling; at 8 GPUs the job is exactly cfg3,
-1B coordinates x 256 peers).  cfg3 itself (1.02 TB of peer data) does not fit
-one GPU's 288 GB, so a GPU owns one 125M-coordinate tile (128 GB resident).
+MI355X.  value = peer-update bytes consumed by all ranks / step time.
 
-A step = one FedAvg pass (sum of K peers in list order, /K, w += 0.1*mean)
-over the resident tile; at N > 1 each rank reduces its round-robin coordinate
-chunks and an RCCL all-gather (over xGMI) reassembles the global model,
-pipelined per chunk on a second stream.  Inputs are generated on device by
-the counter PRNG before timing; nothing is skipped inside the timed region.
+Main line (default): cfg3's per-GPU coordinate tile -- FedAvg over 256 peers
+x 125M fp32 coordinates PER GPU, resident in HBM (128 GB), weak scaling (at 8
+GPUs the job is exactly cfg3, 1B coordinates x 256 peers).  A step = one
+FedAvg pass (sum of K peers in list order, /K, w += 0.1*mean; reference
+aggregator/aggregation.py:15-38) over the tile; at N > 1 each rank reduces its
+round-robin coordinate chunks and an all-gather (RCCL over xGMI) reassembles
+the global model, pipelined per chunk on a second stream.  Inputs are made on
+device by the counter PRNG before timing; nothing is skipped inside the
+timed region.
 
-value = peer-update bytes consumed by all ranks / step time (GB/s).
+Sub-records (the "sub" object of the same line):
+  cfg3_full     the FIXED cfg3 job, 1B coordinates x 256 peers (1.02 TB of
+                peer data), as eight 125M-coordinate tiles: 8/N tiles per
+                GPU, each tile's inputs regenerated outside the timed region
+                (1.02 TB does not fit 288 GB); time = sum of tile kernel times
+                + the all-gathers (reported separately).  Strong scaling.
+  cfg2_dropin   cfg2 through the drop-in boundary: aggregate_models on a
+                ResNet-18 state_dict (62 tensors, 11.7M params) x 64 updates
+                -- the segment-table kernel the reference's caller reaches
+  cfg4_median / cfg4_trimmed / median256 / trimmed256
+                the robust rules at 128 peers x 100M and 256 peers x 100M
+(N = 1 only, except cfg3_full, which runs at every N.)
+
 roofline.achieved = algorithmic bytes per launch 4n(K+2) / mean kernel time
-(HIP events on the launch stream), peak 8.0 TB/s.
+(HIP events on the launch stream), peak 8.0 TB/s; roofline.traffic = HBM
+bytes per launch from rocprofv3 PMC FETCH_SIZE/WRITE_SIZE
+(profiles/traffic_<workload>.json, tools/pmc_traffic.py).
 """
 from __future__ import annotations
 
@@ -24,6 +39,7 @@ import json
 import os
 import sys
 import time
+import types
 
 import torch
 import torch.distributed as dist
@@ -33,12 +49,14 @@ sys.path.insert(0, REPO)
 
 from p2pdl_amd import ops  # noqa: E402
 
+METRIC = "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
 W_PEER, UPD_SCALE, W_SCALE = 0xFFFFF, 1e-2, 5e-2
+CFG3_COORDS, CFG3_TILE = 1_000_000_000, 125_000_000
 
 WORKLOADS = {
     # name: (rule, peers, coords per GPU, seed)
-    "cfg3": ("fedavg", 256, 125_000_000, 0x5EED0002),
+    "cfg3": ("fedavg", 256, CFG3_TILE, 0x5EED0002),
     "cfg2": ("fedavg", 64, 11_689_512, 0x5EED0001),
     "cfg4-median": ("median", 128, 100_000_000, 0x5EED0003),
     "cfg4-trimmed": ("trimmed", 128, 100_000_000, 0x5EED0003),
@@ -55,10 +73,13 @@ WORKLOADS = {
     # cfg1: the reference's default run -- MNIST MLP (models/model.py:6-8), 3
     # peers, the drop-in aggregate_models end to end (latency-bound)
     "cfg1": ("dropin", 3, 535_818, 0x5EED0000),
+    # cfg2 through aggregate_models (ResNet-18 state_dict, segment kernel)
+    "cfg2-dropin": ("dropin", 64, 11_689_512, 0x5EED0001),
     # land 16 serialized ResNet-18-sized updates (11.7M
     # params each) in the device slab vs the reference's pickle.loads
     "inbox": ("inbox", 16, 11_689_512, 0x5EED0007),
 }
+SUB_N1 = ["cfg2-dropin", "cfg4-median", "cfg4-trimmed", "median256", "trimmed256"]
 MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
 
@@ -72,15 +93,402 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
+    ap.add_argument("--job", default="", choices=["", "cfg3-full"],
+                    help="cfg3-full: the fixed 1B x 256 job as the main line (strong scaling)")
     ap.add_argument("--coords", type=int, default=0, help="override coordinates per GPU")
     ap.add_argument("--peers", type=int, default=0, help="override K")
     ap.add_argument("--chunks", type=int, default=8, help="all-gather pipeline chunks per rank (N>1)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--sub-cpu-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sub", action="store_true", help="main line only")
     ap.add_argument("--no-check", action="store_true")
     return ap.parse_args()
 
 
+class Ctx(types.SimpleNamespace):
+    """world / rank / device / dist backend of this process."""
+
+
+def cpu_record(res: dict, unit: str, kind: str, sample: str) -> dict:
+    return {"value": round(res["value"], 3), "unit": unit, "cores": res["threads"], "kind": kind,
+            "sample": sample, "value_1thread": round(res["value_1thread"], 3), "threads": res["threads"],
+            "cpu_count": res["cpu_count"], "affinity": res["affinity"], "threads_rule": res["threads_rule"]}
+
+
+def traffic_for(name: str, coords: int, peers: int):
+    tfile = os.path.join(REPO, "profiles", f"traffic_{name}.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tj = json.load(f)
+        if tj.get("coords_per_launch") == coords and tj.get("peers") == peers:
+            return tj.get("hbm_bytes_per_launch")
+    return None
+
+
+def roofline(alg_bytes: float, kern_ms: float, traffic, **extra) -> dict:
+    ach = alg_bytes / (kern_ms / 1e3) / 1e9
+    return dict({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel_ms": round(kern_ms, 4),
+                 "alg_bytes_per_launch": int(alg_bytes)}, **extra)
+
+
+def parallelism(c: Ctx) -> str:
+    if c.world == 1:
+        return "single GPU"
+    via = "RCCL over xGMI" if c.backend == "nccl" else f"{c.backend} (rehearsal, ranks share one GPU)"
+    return f"coord-shard x{c.world}, all_gather_into_tensor via {via}"
+
+
+def oracle_expect(rule, K, m, seed, chunk=0, nranks=1, rank=0):
+    """First m coordinates of a chunk-mapped workload, from the CPU oracle."""
+    import oracle  # checker only
+
+    peers = [oracle.synth(m, seed, p, UPD_SCALE, chunk, nranks, rank) for p in range(K)]
+    w0 = oracle.synth(m, seed, W_PEER, W_SCALE, chunk, nranks, rank)
+    rid = ops.rule_id(rule)
+    if rid == 0:
+        want, _ = oracle.fedavg(peers, w0)
+    else:
+        want, _ = oracle.robust(peers, rid, ops.trim_count(K) if rid == 2 else 0, w=w0)
+    return want
+
+
+def bits_equal(a, b) -> bool:
+    import numpy as np
+
+    return np.array_equal(np.ascontiguousarray(a, dtype=np.float32).view(np.uint32),
+                          np.ascontiguousarray(b, dtype=np.float32).view(np.uint32))
+
+
+# ------------------------------------------------------------------ flat rules
+def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chunks):
+    """Resident [K, n] slab per rank; a step = the rule over it (+ the chunked
+    all-gather at N > 1).  Returns (record, ms_per_step)."""
+    world, rank, dev = c.world, c.rank, c.dev
+    S = chunks if world > 1 else 1
+    C = -(-n // S)
+    n = C * S  # whole chunks per rank
+    free, _ = torch.cuda.mem_get_info(dev)
+    need = (K + 2 + world) * n * 4
+    if need > free * 0.97:
+        raise SystemExit(f"{name}: needs {need/1e9:.1f} GB, {free/1e9:.1f} GB free")
+    log(f"[rank {rank}] {name}: generating {K} x {n:,} fp32 peer slab ({K*n*4/1e9:.1f} GB)")
+    slab = torch.empty((K, n), dtype=torch.float32, device=dev)
+    for p in range(K):
+        ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE, C, world, rank)
+    w = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.fill_synthetic_(w, seed, W_PEER, W_SCALE, C, world, rank)
+    w_full = torch.empty(n * world, dtype=torch.float32, device=dev) if world > 1 else None
+    tables = [ops.pointer_table([slab[p, s * C:(s + 1) * C] for p in range(K)], dev) for s in range(S)]
+    torch.cuda.synchronize()
+    comp = torch.cuda.current_stream(dev)
+    comm = torch.cuda.Stream(dev)
+    kern = []
+
+    def step(record=False):
+        for s in range(S):
+            ws = w[s * C:(s + 1) * C]
+            if record:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(comp)
+            ops.aggregate(None, rule, w=ws, lr=0.1, table=tables[s])
+            if record:
+                e1.record(comp)
+                kern.append((e0, e1))
+            if world > 1:
+                done = torch.cuda.Event()
+                done.record(comp)
+                comm.wait_event(done)
+                with torch.cuda.stream(comm):
+                    dist.all_gather_into_tensor(w_full[s * C * world:(s + 1) * C * world], ws)
+        if world > 1:
+            comp.wait_stream(comm)
+
+    # correctness spot check of the first warmup step: rank 0 checks the first
+    # m coordinates of EVERY rank's first chunk, in its own w and, at N > 1,
+    # where the all-gather placed them in the global model
+    m = min(4096, C)
+    check = not args.no_check and rank == 0
+    for i in range(max(warmup, 1 if check else 0)):
+        step()
+        if i == 0 and check:
+            torch.cuda.synchronize()
+            bad = [g for g in range(world)
+                   if not bits_equal((w_full[g * C:g * C + m] if world > 1 else w[:m]).cpu().numpy(),
+                                     oracle_expect(rule, K, m, seed, C, world, g))]
+            log(f"[rank 0] {name}: spot check vs oracle ({m} coords x {world} rank chunk(s)): "
+                f"{'bit-exact' if not bad else f'MISMATCH on ranks {bad}'}")
+            if bad:
+                raise SystemExit(f"bench: {name} output differs from the oracle")
+        if world > 1:
+            dist.barrier()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = sum(a.elapsed_time(b) for a, b in kern) / len(kern)
+    del slab, w, w_full, tables
+    torch.cuda.empty_cache()
+    step_s = elapsed / steps
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_s > 0:
+        import oracle.cpu_baseline as cb  # baseline leg only
+
+        if rule == "fedavg":
+            n_s = 1_000_000
+            res = cb.fedavg(K, n_s, cpu_s)
+            what = "reference op sequence (aggregation.py:15-38)"
+        elif rule == "median":
+            n_s = 262_144
+            res = cb.median(K, n_s, cpu_s)
+            what = "torch.median(dim=0) (the build-defined rule on CPU)"
+        else:
+            n_s = 262_144
+            res = cb.trimmed(K, n_s, ops.trim_count(K), cpu_s)
+            what = "torch.sort(dim=0) + ascending sum of the kept ranks (the build-defined rule on CPU)"
+        cpu = cpu_record(res, "GB/s", "port", f"{K} peers x {n_s:,} fp32 coords, {what}, "
+                                              f"{res['reps']} reps in {res['seconds']}s")
+    dtype = "fp32" if rule == "fedavg" else "fp32 (u32 total-order keys)"
+    rec = {
+        "workload": name, "value": round(K * n * 4 * world / step_s / 1e9, 2), "unit": "GB/s",
+        "ms_per_step": round(step_s * 1e3, 4), "steps": steps, "scaling": "weak", "dtype": dtype,
+        "config": {"workload": f"{name}: {rule} over {K} peers x {n:,} fp32 coords per GPU"
+                               + (" (cfg3 per-GPU tile; N=8 -> the 1B-coordinate job)" if name == "cfg3" else ""),
+                   "rule": rule, "peers": K, "coords_per_gpu": n, "coords_total": n * world,
+                   "parallelism": parallelism(c),
+                   "pct_hbm_peak_step": round(4 * n * (K + 2) / step_s / 1e9 / HBM_PEAK_GBS, 4)},
+        "roofline": roofline(4 * C * (K + 2), kern_ms, traffic_for(name, C, K)),
+        "cpu_baseline": cpu,
+    }
+    return rec, step_s
+
+
+# ------------------------------------------------------------------ cfg3 full job
+def measure_cfg3_full(c: Ctx, args, passes=2):
+    """The fixed cfg3 job: 1B coordinates x 256 peers in eight 125M tiles;
+    rank r runs tiles r, r+N, ... (8/N of them).  Per tile: regenerate the
+    tile's 256 peer slices (+ its w slice) outside the timed region, run the
+    FedAvg kernel (HIP events), then at N > 1 all-gather the tile round into
+    the global model (events on the comm stream).  Reported time = sum of
+    tile kernel times + sum of all-gather times, max over ranks."""
+    world, rank, dev = c.world, c.rank, c.dev
+    K, seed, T = 256, WORKLOADS["cfg3"][3], CFG3_TILE
+    ntiles = CFG3_COORDS // T
+    if ntiles % world:
+        raise SystemExit(f"cfg3-full: {ntiles} tiles do not split over {world} GPUs")
+    per = ntiles // world
+    slab = torch.empty((K, T), dtype=torch.float32, device=dev)
+    w = torch.empty(T, dtype=torch.float32, device=dev)
+    w_full = torch.empty(CFG3_COORDS, dtype=torch.float32, device=dev) if world > 1 else None
+    table = ops.pointer_table(list(slab), dev)
+    comp = torch.cuda.current_stream(dev)
+    comm = torch.cuda.Stream(dev)
+    kern_ms, gather_ms = [], []
+    checked = False
+    for _ in range(passes):
+        k_tot = g_tot = 0.0
+        for s in range(per):
+            tile = s * world + rank  # round s: global tile s*N + r (contiguous round in the global model)
+            for p in range(K):
+                ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE, T, ntiles, tile)
+            ops.fill_synthetic_(w, seed, W_PEER, W_SCALE, T, ntiles, tile)
+            if world > 1:
+                dist.barrier()
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            e[0].record(comp)
+            ops.aggregate(None, "fedavg", w=w, lr=0.1, table=table)
+            e[1].record(comp)
+            if world > 1:
+                comm.wait_event(e[1])
+                with torch.cuda.stream(comm):
+                    e[2].record(comm)
+                    dist.all_gather_into_tensor(w_full[s * world * T:(s + 1) * world * T], w)
+                    e[3].record(comm)
+                comp.wait_stream(comm)
+            torch.cuda.synchronize()
+            k_tot += e[0].elapsed_time(e[1])
+            if world > 1:
+                g_tot += e[2].elapsed_time(e[3])
+            if not checked and not args.no_check and rank == 0:
+                m = 4096
+                got = (w_full[s * world * T:s * world * T + m] if world > 1 else w[:m]).cpu().numpy()
+                ok = bits_equal(got, oracle_expect("fedavg", K, m, seed, T, ntiles, s * world))
+                log(f"[rank 0] cfg3-full: spot check of tile {s * world} vs oracle: {'bit-exact' if ok else 'MISMATCH'}")
+                if not ok:
+                    raise SystemExit("bench: cfg3-full differs from the oracle")
+                checked = True
+        kern_ms.append(k_tot)
+        gather_ms.append(g_tot)
+    k_ms, g_ms = min(kern_ms), min(gather_ms)  # best pass (each pass is the whole job)
+    if world > 1:
+        t = torch.tensor([k_ms + g_ms, k_ms, g_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tot, k_ms, g_ms = (float(x) for x in t.tolist())
+    else:
+        tot = k_ms
+    del slab, w, w_full, table
+    torch.cuda.empty_cache()
+    peer_bytes = K * CFG3_COORDS * 4
+    return {
+        "workload": "cfg3_full", "value": round(peer_bytes / (tot / 1e3) / 1e9, 2), "unit": "GB/s",
+        "ms_per_job": round(tot, 3), "kernel_ms_sum": round(k_ms, 3), "allgather_ms_sum": round(g_ms, 3),
+        "scaling": "strong", "dtype": "fp32",
+        "config": {"workload": f"cfg3 full job: fedavg over {K} peers x {CFG3_COORDS:,} fp32 coords "
+                               f"({peer_bytes/1e12:.3f} TB) as {ntiles} tiles of {T:,}; {per} tile(s) per GPU",
+                   "tiles_per_gpu": per, "parallelism": parallelism(c),
+                   "timing": "sum of per-tile kernel times (HIP events) + all-gather times; inputs "
+                             "regenerated per tile outside the timed region (1.02 TB > 288 GB HBM)"},
+        "roofline": roofline(4 * T * (K + 2), k_ms / per, traffic_for("cfg3", T, K)),
+    }
+
+
+# ------------------------------------------------------------------ drop-in (cfg1 / cfg2)
+MLP_SHAPES = [("fc1.weight", (512, 784)), ("fc1.bias", (512,)), ("fc2.weight", (256, 512)),
+              ("fc2.bias", (256,)), ("fc3.weight", (10, 256)), ("fc3.bias", (10,))]  # models/model.py:6-8
+
+
+def resnet18_param_shapes():
+    """The 62 parameter tensors of torchvision's ResNet-18 (11,689,512 fp32)."""
+    shapes = [("conv1.weight", (64, 3, 7, 7)), ("bn1.weight", (64,)), ("bn1.bias", (64,))]
+    cin = 64
+    for li, cout in enumerate((64, 128, 256, 512), start=1):
+        for blk in range(2):
+            p = f"layer{li}.{blk}."
+            c0 = cin if blk == 0 else cout
+            shapes += [(p + "conv1.weight", (cout, c0, 3, 3)), (p + "bn1.weight", (cout,)), (p + "bn1.bias", (cout,)),
+                       (p + "conv2.weight", (cout, cout, 3, 3)), (p + "bn2.weight", (cout,)), (p + "bn2.bias", (cout,))]
+            if blk == 0 and cin != cout:
+                shapes += [(p + "downsample.0.weight", (cout, cin, 1, 1)), (p + "downsample.1.weight", (cout,)),
+                           (p + "downsample.1.bias", (cout,))]
+        cin = cout
+    return shapes + [("fc.weight", (1000, 512)), ("fc.bias", (1000,))]
+
+
+def _numel(shape):
+    out = 1
+    for s in shape:
+        out *= s
+    return out
+
+
+def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
+    """aggregate_models (reference aggregator/aggregation.py:7-46) on a fake
+    Node, end to end: host segment table + one kernel launch per call.
+    Updates are rows of a [K, N] device slab, as DeviceInbox lands them."""
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    dev = c.dev
+    shapes = MLP_SHAPES if name == "cfg1" else resnet18_param_shapes()
+    sizes = [_numel(s) for _, s in shapes]
+    n = sum(sizes)
+    offs = [0]
+    for sz in sizes:
+        offs.append(offs[-1] + sz)
+    model = torch.nn.Module()
+    for i, (nm, shape) in enumerate(shapes):
+        model.register_parameter(nm.replace(".", "__"), torch.nn.Parameter(
+            torch.empty(shape, dtype=torch.float32, device=dev), requires_grad=False))
+    flat_w = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.fill_synthetic_(flat_w, seed, W_PEER, W_SCALE)
+    with torch.no_grad():
+        for i, p in enumerate(model.parameters()):
+            p.view(-1).copy_(flat_w[offs[i]:offs[i + 1]])
+    slab = torch.empty((K, n), dtype=torch.float32, device=dev)
+    for p in range(K):
+        ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE)
+    keys = [nm.replace(".", "__") for nm, _ in shapes]
+    updates = [{k: slab[j, offs[i]:offs[i + 1]].view(shapes[i][1]) for i, k in enumerate(keys)} for j in range(K)]
+    node = types.SimpleNamespace(model=model, trainers_list=[0] * K, addr="127.0.0.1", port=1, neighbors=[],
+                                 received_models=[])
+    saved = agg.broadcast_global_model_update
+    agg.broadcast_global_model_update = lambda self: None  # networking is out of scope
+    comp = torch.cuda.current_stream(dev)
+    ev = []
+
+    def call(record=False):
+        node.received_models.extend({"model": u, "sender": j} for j, u in enumerate(updates))
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(comp)
+        agg.aggregate_models(node)
+        if record:
+            e1.record(comp)
+            ev.append((e0, e1))
+
+    try:
+        call()
+        torch.cuda.synchronize()
+        if not args.no_check:
+            import oracle  # checker only
+
+            m = min(n, 4096)
+            got = torch.cat([p.detach().reshape(-1) for p in model.parameters()])[:m].cpu().numpy()
+            want, _ = oracle.fedavg([oracle.synth(m, seed, p, UPD_SCALE) for p in range(K)],
+                                    oracle.synth(m, seed, W_PEER, W_SCALE))
+            ok = bits_equal(got, want)
+            log(f"{name}: drop-in spot check vs oracle ({m} coords): {'bit-exact' if ok else 'MISMATCH'}")
+            if not ok:
+                raise SystemExit(f"bench: {name} drop-in differs from the oracle")
+        for _ in range(max(warmup, 2)):
+            call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call(record=True)
+        torch.cuda.synchronize()
+        step_s = (time.perf_counter() - t0) / steps
+    finally:
+        agg.broadcast_global_model_update = saved
+    call_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    # the same bytes through the flat C-ABI kernel (one buffer per peer), for comparison
+    table = ops.pointer_table(list(slab), dev)
+    fe = []
+    for i in range(steps + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(comp)
+        ops.aggregate(None, "fedavg", w=flat_w, lr=0.1, table=table)
+        e1.record(comp)
+        if i >= 2:
+            fe.append((e0, e1))
+    torch.cuda.synchronize()
+    flat_ms = sum(a.elapsed_time(b) for a, b in fe) / len(fe)
+    del slab, flat_w, table, updates, model
+    torch.cuda.empty_cache()
+    cpu = None
+    if not args.no_cpu_baseline and cpu_s > 0:
+        import oracle.cpu_baseline as cb  # baseline leg only
+
+        res = cb.fedavg_state_dict(K, sizes, cpu_s, seed)
+        cpu = cpu_record(res, "GB/s", "port", f"{len(sizes)}-tensor state_dict ({n:,} params) x {K} updates, "
+                                              f"reference per-key op sequence (aggregation.py:15-38) on torch "
+                                              f"CPU, {res['reps']} reps in {res['seconds']}s")
+    return {
+        "workload": name.replace("-", "_"), "value": round(K * n * 4 / step_s / 1e9, 2), "unit": "GB/s",
+        "ms_per_step": round(step_s * 1e3, 4), "us_per_call": round(step_s * 1e6, 1), "steps": steps,
+        "scaling": "weak", "dtype": "fp32",
+        "config": {"workload": f"{name}: drop-in aggregate_models, {len(sizes)}-tensor state_dict "
+                               f"({n:,} params) x {K} updates, one segment-table launch per call",
+                   "peers": K, "coords_per_gpu": n, "tensors": len(sizes), "parallelism": "single GPU"},
+        "roofline": roofline(4 * n * (K + 2), call_ms, traffic_for(name, n, K),
+                             timing="HIP events around aggregate_models (table H2D + segment kernel)",
+                             flat_kernel_ms=round(flat_ms, 4),
+                             vs_flat_kernel=round(flat_ms / call_ms, 4)),
+        "cpu_baseline": cpu,
+    }
+
+
+# ------------------------------------------------------------------ digest (cfg5 / sha256)
 def run_digest_workload(args, rule, K, n, seed, dev):
     """cfg5 / sha256: one process, one GPU (replicas only: see DESIGN.md)."""
     import hashlib
@@ -97,9 +505,8 @@ def run_digest_workload(args, rule, K, n, seed, dev):
         payload = buf[p * stride + MSG_HEADER:p * stride + msg_bytes].view(torch.float32)
         ops.fill_synthetic_(payload, seed, p, UPD_SCALE)
     offsets = [p * stride for p in range(K)]
-    lens = [msg_bytes] * K
     ptrs = torch.tensor([buf.data_ptr() + o for o in offsets], dtype=torch.int64, device=dev)
-    lens_d = torch.tensor(lens, dtype=torch.int64, device=dev)
+    lens_d = torch.tensor([msg_bytes] * K, dtype=torch.int64, device=dev)
     digests = torch.empty((K, 32), dtype=torch.uint8, device=dev)
     lib = ops.N.lib()
 
@@ -110,8 +517,7 @@ def run_digest_workload(args, rule, K, n, seed, dev):
     digest()
     expected = digests.clone()  # what the senders signed (untimed)
     torch.cuda.synchronize()
-    # cross-check two digests on the host (checker only)
-    for p in (0, K - 1):
+    for p in (0, K - 1):  # cross-check two digests on the host (checker only)
         assert bytes(digests[p].cpu().numpy()) == hashlib.sha256(
             bytes(buf[offsets[p]:offsets[p] + msg_bytes].cpu().numpy())).digest(), "sha256 mismatch"
     log("digest spot check vs hashlib: ok")
@@ -149,8 +555,7 @@ def run_digest_workload(args, rule, K, n, seed, dev):
     for _ in range(args.steps):
         step(record=True)
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    step_s = el / args.steps
+    step_s = (time.perf_counter() - t0) / args.steps
     sha_ms = sum(a.elapsed_time(b) for a, b, _ in kern) / len(kern)
     agg_ms = sum(b.elapsed_time(c) for _, b, c in kern) / len(kern)
     hashed = K * msg_bytes
@@ -158,24 +563,22 @@ def run_digest_workload(args, rule, K, n, seed, dev):
     agg_bytes = 4 * n * (acc + 2) if rule == "fused" else 0
     cpu = None
     if not args.no_cpu_baseline:
-        from concurrent.futures import ThreadPoolExecutor
+        import oracle.cpu_baseline as cb  # baseline leg only
 
-        thr = int(os.environ.get("OMP_NUM_THREADS", "16"))
-        sample = [bytes(buf[offsets[p]:offsets[p] + min(msg_bytes, 16 << 20)].cpu().numpy()) for p in range(min(K, 32))]
-        t0 = time.perf_counter()
-        reps = 0
-        with ThreadPoolExecutor(thr) as ex:  # hashlib releases the GIL
-            while time.perf_counter() - t0 < args.cpu_seconds:
-                list(ex.map(lambda m: hashlib.sha256(m).digest(), sample))
-                reps += 1
-        ce = time.perf_counter() - t0
-        cpu = {"value": round(sum(map(len, sample)) * reps / ce / 1e9, 3), "unit": "GB/s", "cores": thr,
-               "kind": "port", "sample": f"hashlib.sha256 (OpenSSL, the function behind reference "
-                                         f"utils/crypto.py:56) over {len(sample)} x {len(sample[0]):,} B, "
-                                         f"{thr} threads, {reps} reps"}
-    line = {
-        "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
-        "value": round(hashed / step_s / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        sample = [bytes(buf[offsets[p]:offsets[p] + min(msg_bytes, 16 << 20)].cpu().numpy()) for p in range(min(K, 64))]
+        res = cb.sha256(sample, args.cpu_seconds)
+        what = (f"hashlib.sha256 (OpenSSL, the function behind reference utils/crypto.py:56) over "
+                f"{len(sample)} x {len(sample[0]):,} B")
+        if rule == "fused":
+            # end to end on the host: hash every message, then the reference's
+            # FedAvg op sequence over the accepted payloads (GB/s of hashed bytes)
+            fed = cb.fedavg(acc, 1_000_000, max(2.0, args.cpu_seconds / 3))
+            host_s = hashed / (res["value"] * 1e9) + agg_bytes / 4 / (acc + 2) * acc / (fed["value"] * 1e9)
+            res = dict(res, value=hashed / host_s / 1e9, value_1thread=res["value_1thread"])
+            what += f" + reference FedAvg ops over {acc} accepted (host, {fed['value']:.1f} GB/s)"
+        cpu = cpu_record(res, "GB/s", "port", f"{what}, {res['reps']} reps in {res['seconds']}s")
+    print(json.dumps({
+        "metric": METRIC, "value": round(hashed / step_s / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32 (SHA-256) + fp32",
         "data": "synthetic serialized updates (64-B header + device-PRNG fp32 payload)",
@@ -191,15 +594,13 @@ def run_digest_workload(args, rule, K, n, seed, dev):
                      # 2.4 GHz, ~910 instructions per 64-B block on the chain
                      "chain_issue_bound_gbs": round(min(K, 65536) * 64 / (910 * 4 / 2.4e9) / 1e9, 2)},
         "cpu_baseline": cpu,
-    }
-    print(json.dumps(line), flush=True)
+    }), flush=True)
 
 
+# ------------------------------------------------------------------ delta / inbox
 def run_delta_workload(args, n, seed, dev):
     """Trainer-side local update (reference node/node.py:273-282) of one
     flat n-parameter model: delta = cur - prev; prev = cur.  One GPU."""
-    import numpy as np
-
     cur = torch.empty(n, dtype=torch.float32, device=dev)
     prev = torch.empty_like(cur)
     delta = torch.empty_like(cur)
@@ -213,8 +614,7 @@ def run_delta_workload(args, n, seed, dev):
         ops.delta_snapshot_(cur, prev, delta)
         torch.cuda.synchronize()
         want, _ = oracle.delta_snapshot_np(oracle.synth(m, seed, 1, 1e-1), oracle.synth(m, seed, 2, 1e-1))
-        ok = np.array_equal(delta[:m].cpu().numpy().view(np.uint32), want.view(np.uint32)) and \
-            torch.equal(prev[:m], cur[:m])
+        ok = bits_equal(delta[:m].cpu().numpy(), want) and torch.equal(prev[:m], cur[:m])
         log(f"spot check vs oracle ({m} coords): {'bit-exact' if ok else 'MISMATCH'}")
         if not ok:
             raise SystemExit("bench: delta kernel differs from the oracle")
@@ -233,122 +633,23 @@ def run_delta_workload(args, n, seed, dev):
     step_s = (time.perf_counter() - t0) / args.steps
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     alg = 16 * n
-    traffic = None
-    tfile = os.path.join(REPO, "profiles", "traffic_delta.json")
-    if os.path.exists(tfile):
-        with open(tfile) as f:
-            tj = json.load(f)
-        if tj.get("coords_per_launch") == n:
-            traffic = tj.get("hbm_bytes_per_launch")
     cpu = None
     if not args.no_cpu_baseline:
         import oracle.cpu_baseline as cb  # baseline leg only
 
-        torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
         n_s = 50_000_000
-        gbs, thr, reps, el = cb.time_delta(n_s, args.cpu_seconds)
-        cpu = {"value": round(gbs, 3), "unit": "GB/s", "cores": thr, "kind": "port",
-               "sample": f"{n_s:,} fp32 params, reference ops cur - prev and clone (node/node.py:279,282) "
-                         f"on torch CPU, {reps} reps in {el:.1f}s"}
+        res = cb.delta(n_s, args.cpu_seconds)
+        cpu = cpu_record(res, "GB/s", "port", f"{n_s:,} fp32 params, reference ops cur - prev and clone "
+                                              f"(node/node.py:279,282) on torch CPU, {res['reps']} reps")
     print(json.dumps({
-        "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
-        "value": round(alg / step_s / 1e9, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "metric": METRIC, "value": round(alg / step_s / 1e9, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (device counter PRNG); value = algorithmic bytes (16 B/param) per second",
         "config": {"workload": f"delta: trainer local update over {n:,} fp32 params (SURVEY §8(f) row 2)",
                    "coords_per_gpu": n, "parallelism": "single GPU (replicas only)"},
-        "roofline": {"bound": "hbm", "achieved": round(alg / (kern_ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(alg / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg},
+        "roofline": dict(roofline(alg, kern_ms, None), traffic=traffic_for("delta", n, 1)),
         "cpu_baseline": cpu}), flush=True)
-
-
-MLP_SHAPES = [("fc1.weight", (512, 784)), ("fc1.bias", (512,)), ("fc2.weight", (256, 512)),
-              ("fc2.bias", (256,)), ("fc3.weight", (10, 256)), ("fc3.bias", (10,))]  # models/model.py:6-8
-
-
-def run_dropin_workload(args, K, seed, dev):
-    """cfg1: one call of the drop-in aggregate_models (reference
-    aggregator/aggregation.py:7-46) on the MNIST MLP with K updates, host
-    table building included -- latency, reported as us per call."""
-    import types
-
-    from p2pdl_amd.aggregator import aggregation as agg
-
-    agg_bc = agg.broadcast_global_model_update
-    agg.broadcast_global_model_update = lambda self: None  # networking is out of scope
-    model = torch.nn.Module()
-    n = 0
-    for name, shape in MLP_SHAPES:
-        mod, attr = name.split(".")
-        if not hasattr(model, mod):
-            model.add_module(mod, torch.nn.Module())
-        t = torch.empty(shape, dtype=torch.float32, device=dev)
-        ops.fill_synthetic_(t.view(-1), seed, W_PEER, W_SCALE)
-        getattr(model, mod).register_parameter(attr, torch.nn.Parameter(t, requires_grad=False))
-        n += t.numel()
-    updates = []
-    for p in range(K):
-        upd = {}
-        for name, shape in MLP_SHAPES:
-            t = torch.empty(shape, dtype=torch.float32, device=dev)
-            ops.fill_synthetic_(t.view(-1), seed, p, UPD_SCALE)
-            upd[name] = t
-        updates.append(upd)
-    node = types.SimpleNamespace(model=model, trainers_list=[0] * K, addr="127.0.0.1", port=1, neighbors=[],
-                                 received_models=[])
-
-    def call():
-        node.received_models.extend({"model": u, "sender": j} for j, u in enumerate(updates))
-        agg.aggregate_models(node)
-
-    for _ in range(max(args.warmup, 3)):
-        call()
-    torch.cuda.synchronize()
-    steps = max(args.steps, 100)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        call()
-    torch.cuda.synchronize()
-    us = (time.perf_counter() - t0) / steps * 1e6
-    agg.broadcast_global_model_update = agg_bc
-    cpu = None
-    if not args.no_cpu_baseline:
-        import oracle.cpu_baseline as cb  # baseline leg only
-
-        torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
-        ws = [torch.zeros(s) for _, s in MLP_SHAPES]
-        peers = [[torch.rand(s) for _, s in MLP_SHAPES] for _ in range(K)]
-        reps, t1 = 0, time.perf_counter()
-        while time.perf_counter() - t1 < min(args.cpu_seconds, 3.0):
-            for l, w in enumerate(ws):  # the reference's per-key op sequence (aggregation.py:15-38)
-                cb.reference_ops_fedavg_(w, [p[l] for p in peers])
-            reps += 1
-        cus = (time.perf_counter() - t1) / reps * 1e6
-        cpu = {"value": round(cus, 1), "unit": "us per aggregation", "cores": torch.get_num_threads(),
-               "kind": "port", "sample": f"MLP state_dict ({n:,} params) x {K} updates, reference op sequence "
-                                         f"per key on torch CPU, {reps} reps"}
-    print(json.dumps({
-        "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
-        "value": round(K * n * 4 / (us * 1e-6) / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": steps,
-        "warmup": args.warmup, "ms_per_step": round(us / 1e3, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic MLP weights and updates (device PRNG)",
-        "config": {"workload": f"cfg1: drop-in aggregate_models, MNIST MLP ({n:,} params) x {K} updates, "
-                               f"latency-bound (us_per_call)", "us_per_call": round(us, 1),
-                   "parallelism": "single GPU"},
-        "roofline": None, "cpu_baseline": cpu}), flush=True)
-
-
-def _resnet18_like_shapes(total):
-    """Tensor sizes of a ResNet-18 state_dict (conv/fc weights, BN vectors),
-    the last one padded so the parameters add up to `total`."""
-    sizes = [64 * 3 * 49] + [64] * 2 + [64 * 64 * 9] * 4 + [64] * 8 + [128 * 64 * 9, 128 * 128 * 9, 128 * 64]
-    sizes += [128 * 128 * 9] * 2 + [128] * 10 + [256 * 128 * 9, 256 * 256 * 9, 256 * 128] + [256 * 256 * 9] * 2
-    sizes += [256] * 10 + [512 * 256 * 9, 512 * 512 * 9, 512 * 256] + [512 * 512 * 9] * 2 + [512] * 10
-    sizes += [1000 * 512, 1000]
-    sizes[-2] += total - sum(sizes)
-    return sizes
 
 
 def run_inbox_workload(args, K, n, seed, dev):
@@ -360,17 +661,17 @@ def run_inbox_workload(args, K, n, seed, dev):
 
     from p2pdl_amd.node.inbox import DeviceInbox
 
-    sizes = _resnet18_like_shapes(n)
-    keys = [f"layer{i}.weight" for i in range(len(sizes))]
+    shapes = resnet18_param_shapes()
+    keys = [nm for nm, _ in shapes]
     ser = []
     for p in range(K):
         upd = {}
-        for i, (k, m) in enumerate(zip(keys, sizes)):
-            t = torch.empty(m, dtype=torch.float32, device=dev)
-            ops.fill_synthetic_(t, seed, p * 1000 + i, UPD_SCALE)
+        for i, (k, s) in enumerate(shapes):
+            t = torch.empty(s, dtype=torch.float32, device=dev)
+            ops.fill_synthetic_(t.view(-1), seed, p * 1000 + i, UPD_SCALE)
             upd[k] = t
         ser.append(pickle.dumps(upd))  # what a CUDA trainer sends
-    template = {k: torch.empty(m, dtype=torch.float32, device=dev) for k, m in zip(keys, sizes)}
+    template = {k: torch.empty(s, dtype=torch.float32, device=dev) for k, s in shapes}
     inbox = DeviceInbox(template, k_max=K, device=dev)
     if not args.no_check:
         got = inbox.land(ser[0], 0)
@@ -401,13 +702,13 @@ def run_inbox_workload(args, K, n, seed, dev):
             pickle.loads(s)
 
     t_ours, t_ref = timed(ours), timed(reference)
+    n = sum(_numel(s) for _, s in shapes)
     nbytes = K * n * 4
     print(json.dumps({
-        "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
-        "value": round(nbytes / t_ours / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "metric": METRIC, "value": round(nbytes / t_ours / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(t_ours * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic ResNet-18-sized updates pickled from CUDA tensors",
-        "config": {"workload": f"inbox: land {K} serialized updates of {n:,} params ({len(sizes)} tensors) "
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic ResNet-18 updates pickled from CUDA tensors",
+        "config": {"workload": f"inbox: land {K} serialized updates of {n:,} params ({len(shapes)} tensors) "
                                f"in the device slab (SURVEY §8(f) row 1)", "reference_pickle_loads_gbs":
                    round(nbytes / t_ref / 1e9, 3), "reference_ms": round(t_ref * 1e3, 3),
                    "parallelism": "single GPU, host-to-device"},
@@ -416,6 +717,7 @@ def run_inbox_workload(args, K, n, seed, dev):
         "cpu_baseline": None}), flush=True)
 
 
+# ------------------------------------------------------------------ main
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -434,163 +736,58 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    c = Ctx(world=world, rank=rank, dev=dev, backend=backend)
 
     rule, K, n, seed = WORKLOADS[args.workload]
     K = args.peers or K
     n = args.coords or n
+    one_gpu = {"fused": "cfg5/sha256 run as replicas only", "sha256": "cfg5/sha256 run as replicas only",
+               "delta": "delta runs as replicas only", "inbox": "inbox runs on one GPU", "dropin": "drop-in runs on one GPU"}
+    if rule in one_gpu and world > 1:
+        raise SystemExit(one_gpu[rule] + " (one process per GPU)")
     if rule in ("fused", "sha256"):
-        if world > 1:
-            raise SystemExit("cfg5/sha256 run as replicas only (one process per GPU)")
         return run_digest_workload(args, rule, K, n, seed, dev)
     if rule == "delta":
-        if world > 1:
-            raise SystemExit("delta runs as replicas only (one process per GPU)")
         return run_delta_workload(args, n, seed, dev)
     if rule == "inbox":
-        if world > 1:
-            raise SystemExit("inbox runs on one GPU")
         return run_inbox_workload(args, K, n, seed, dev)
-    if rule == "dropin":
-        if world > 1:
-            raise SystemExit("cfg1 runs on one GPU")
-        return run_dropin_workload(args, K, seed, dev)
-    S = args.chunks if world > 1 else 1
-    C = -(-n // S)
-    n = C * S  # whole chunks per rank
-    free, total = torch.cuda.mem_get_info(dev)
-    need = (K + 2 + world) * n * 4
-    if need > free * 0.97:
-        raise SystemExit(f"workload needs {need/1e9:.1f} GB, {free/1e9:.1f} GB free")
 
-    # ---- synthetic inputs, resident in HBM (outside the timed region) ----
-    log(f"[rank {rank}] generating {K} x {n:,} fp32 peer slab ({K*n*4/1e9:.1f} GB)")
-    slab = torch.empty((K, n), dtype=torch.float32, device=dev)
-    for p in range(K):
-        ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE, C, world, rank)
-    w = torch.empty(n, dtype=torch.float32, device=dev)
-    ops.fill_synthetic_(w, seed, W_PEER, W_SCALE, C, world, rank)
-    w_full = torch.empty(n * world, dtype=torch.float32, device=dev) if world > 1 else None
-    tables = [ops.pointer_table([slab[p, s * C:(s + 1) * C] for p in range(K)], dev) for s in range(S)]
-    torch.cuda.synchronize()
-
-    comp = torch.cuda.current_stream(dev)
-    comm = torch.cuda.Stream(dev)
-    kern_events = []  # (start, end) per kernel launch, on the launch stream
-
-    def step(record=False):
-        for s in range(S):
-            ws = w[s * C:(s + 1) * C]
-            if record:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(comp)
-            ops.aggregate(None, rule, w=ws, lr=0.1, table=tables[s])
-            if record:
-                e1.record(comp)
-                kern_events.append((e0, e1))
-            if world > 1:
-                done = torch.cuda.Event()
-                done.record(comp)
-                comm.wait_event(done)
-                with torch.cuda.stream(comm):
-                    dist.all_gather_into_tensor(w_full[s * C * world:(s + 1) * C * world], ws)
-        if world > 1:
-            comp.wait_stream(comm)
-
-    # ---- correctness spot check of the first warmup step vs the oracle ----
-    # rank 0 checks the first m coordinates of EVERY rank's first chunk: in its
-    # own w and, at N > 1, where the all-gather placed them in the global model
-    m = min(4096, C)
-    check = not args.no_check and rank == 0
-    for i in range(max(args.warmup, 1 if check else 0)):
-        step()
-        if i == 0 and check:
-            torch.cuda.synchronize()
-            import numpy as np
-
-            import oracle  # checker only
-            rid = ops.rule_id(rule)
-            bad = []
-            for g in range(world):
-                peers = [oracle.synth(m, seed, p, UPD_SCALE, C, world, g) for p in range(K)]
-                w0 = oracle.synth(m, seed, W_PEER, W_SCALE, C, world, g)
-                if rid == 0:
-                    want, _ = oracle.fedavg(peers, w0)
-                else:
-                    want, _ = oracle.robust(peers, rid, ops.trim_count(K) if rid == 2 else 0, w=w0)
-                got = (w_full[g * C:g * C + m] if world > 1 else w[:m]).cpu().numpy()
-                if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
-                    bad.append(g)
-            log(f"[rank 0] spot check vs oracle ({m} coords x {world} rank chunk(s)): "
-                f"{'bit-exact' if not bad else f'MISMATCH on ranks {bad}'}")
-            if bad:
-                raise SystemExit("bench: kernel output differs from the oracle")
-        if world > 1:
-            dist.barrier()
-
-    # ---- timed region ----
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(record=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kern_ms = sum(a.elapsed_time(b) for a, b in kern_events) / len(kern_events)
-
-    step_s = elapsed / args.steps
-    peer_bytes = K * n * 4 * world
-    value = peer_bytes / step_s / 1e9
-    launch_n = C
-    alg_bytes = 4 * launch_n * (K + 2)
-    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-
-    traffic = None
-    tfile = os.path.join(REPO, "profiles", f"traffic_{args.workload}.json")
-    if os.path.exists(tfile):
-        with open(tfile) as f:
-            tj = json.load(f)
-        if tj.get("coords_per_launch") == launch_n and tj.get("peers") == K:
-            traffic = tj.get("hbm_bytes_per_launch")
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import oracle.cpu_baseline as cb  # baseline leg only
-
-        torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
-        n_s = 1_000_000
-        if rule == "fedavg":
-            gbs, thr, reps, el = cb.time_fedavg(K, n_s, args.cpu_seconds)
+    data = "synthetic (device counter PRNG, SURVEY.md §8(d)); random-init model weights"
+    if args.job == "cfg3-full":
+        rec = measure_cfg3_full(c, args, passes=max(1, args.steps))
+        main_rec, steps, step_ms = rec, 1, rec["ms_per_job"]
+        sub = {}
+    else:
+        if rule == "dropin":
+            main_rec = measure_dropin(c, args, args.workload, K, seed, max(args.steps, 20), args.warmup,
+                                      args.cpu_seconds)
+            step_ms = main_rec["ms_per_step"]
         else:
-            gbs, thr, reps, el = cb.time_median(K, n_s, args.cpu_seconds)
-        what = ("reference op sequence (aggregation.py:15-38)" if rule == "fedavg"
-                else "torch.median(dim=0) (the build-defined rule on CPU)")
-        cpu = {"value": round(gbs, 3), "unit": "GB/s", "cores": thr, "kind": "port",
-               "sample": f"{K} peers x {n_s:,} fp32 coords, {what} on torch CPU, {reps} reps in {el:.1f}s"}
-
+            main_rec, step_s = measure_flat(c, args, args.workload, rule, K, n, seed, args.steps, args.warmup,
+                                            args.cpu_seconds, args.chunks)
+            step_ms = step_s * 1e3
+        steps = main_rec["steps"]
+        sub = {}
+        if not args.no_sub and args.workload == "cfg3" and not (args.coords or args.peers):
+            sub["cfg3_full"] = measure_cfg3_full(c, args)
+            if world == 1:
+                for name in SUB_N1:
+                    r, k2, n2, s2 = WORKLOADS[name]
+                    if r == "dropin":
+                        rec = measure_dropin(c, args, name, k2, s2, 30, 2, args.sub_cpu_seconds)
+                    else:
+                        rec, _ = measure_flat(c, args, name, r, k2, n2, s2, 10, 2, args.sub_cpu_seconds, 1)
+                    sub[rec["workload"]] = rec
     if rank == 0:
         line = {
-            "metric": "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X",
-            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic (device counter PRNG, SURVEY.md §8(d)); random-init model weights",
-            "config": {"workload": f"{args.workload}: {rule} over {K} peers x {n:,} fp32 coords per GPU"
-                                   + (" (cfg3 per-GPU tile; N=8 -> 1B coords)" if args.workload == "cfg3" else ""),
-                       "rule": rule, "peers": K, "coords_per_gpu": n, "coords_total": n * world,
-                       "parallelism": f"coord-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
-                       "pct_hbm_peak_step": round(4 * n * (K + 2) * world / step_s / 1e9 / world / HBM_PEAK_GBS, 4)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
-            "cpu_baseline": cpu,
+            "metric": METRIC, "value": main_rec["value"], "unit": "GB/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(step_ms, 4), "higher_is_better": True,
+            "scaling": main_rec["scaling"], "vs_baseline": None, "dtype": main_rec["dtype"], "data": data,
+            "config": main_rec["config"], "roofline": main_rec["roofline"],
+            "cpu_baseline": main_rec.get("cpu_baseline"),
         }
+        if sub:
+            line["sub"] = sub
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

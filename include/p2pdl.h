@@ -59,7 +59,9 @@ int32_t p2p_abi_version(void);
 const char *p2p_strerror(int32_t code);
 
 /* Elements per tile of the segment kernel for `rule` with k peers (host
- * planning helper for p2p_segment_t.tile_begin). */
+ * planning helper for p2p_segment_t.tile_begin).  A pure function of
+ * (rule, k): FedAvg 1024; median / trimmed 128 for k <= 128, 64 for
+ * k in 129..256. */
 int64_t p2p_tile_elems(int32_t rule, int32_t k);
 
 /* ---- K1: FedAvg --------------------------------------------------------
@@ -79,7 +81,9 @@ int32_t p2p_fedavg_apply_devk_f32(const float *const *peers, const int32_t *k_de
 /* ---- K2: robust rules (build-defined: reference README.md:10 TODO) -----
  * median: rank (K-1)/2 under the IEEE total order on float bits.
  * trimmed: ascending fp32 sum of sorted ranks b..K-b-1 from +0, / (K-2b).
- * k <= 256. */
+ * k <= 256.  Kernel family (fixed per k, no process state): one lane per
+ * coordinate for k <= 128; 4 lanes x 64 keys, peer rows LDS-DMA staged, for
+ * k in 129..256. */
 int32_t p2p_median_f32(const float *const *peers, int32_t k, int64_t n, float *out,
                        p2p_stream_t stream);
 int32_t p2p_trimmed_mean_f32(const float *const *peers, int32_t k, int64_t n, int32_t trim_b,
@@ -98,14 +102,6 @@ int32_t p2p_aggregate_f32(const float *const *peers, int32_t k, int64_t n, int32
 int32_t p2p_aggregate_segments_f32(const p2p_segment_t *segs, int32_t nseg, int64_t total_tiles,
                                    int32_t k, int32_t rule, int32_t trim_b, float lr,
                                    p2p_stream_t stream);
-
-/* Tuning knob (process-wide, not thread-safe against concurrent launches):
- * kernel layout for robust rules with 65 <= k <= 256.  0 = default (fastest
- * measured per k), 1 = LDS-DMA staged 4 lanes per coordinate for every k,
- * 2 = same with 2 lanes x 64 keys at k <= 128, 3 = the one-lane / 4-wave
- * group kernels, 4 = one lane x 128 keys LDS-DMA staged at k <= 128.  Results are identical; tile sizes (p2p_tile_elems) follow
- * the layout, so segment tables must be built after choosing it. */
-int32_t p2p_set_robust_layout(int32_t layout);
 
 /* w += lr * agg, multiply and add separately rounded (aggregation.py:36-38). */
 int32_t p2p_apply_f32(float *w, const float *agg, float lr, int64_t n, p2p_stream_t stream);

@@ -24,7 +24,7 @@ EXPORTS = (
     "p2p_median_f32", "p2p_trimmed_mean_f32", "p2p_aggregate_f32",
     "p2p_aggregate_segments_f32", "p2p_apply_f32",
     "p2p_sha256_batch", "p2p_digest_accept", "p2p_fill_synthetic_f32",
-    "p2p_set_robust_layout", "p2p_delta_snapshot_f32", "p2p_delta_snapshot_segments_f32",
+    "p2p_delta_snapshot_f32", "p2p_delta_snapshot_segments_f32",
 )
 
 
@@ -57,7 +57,6 @@ _SIGS = {
     "p2p_sha256_batch": ([_P, _P, _I32, _P, _P], _I32),
     "p2p_digest_accept": ([_P, _P, _P, _I32, _P, _P, _P], _I32),
     "p2p_fill_synthetic_f32": ([_P, _I64, _U64, _I32, _F32, _I64, _I32, _I32, _P], _I32),
-    "p2p_set_robust_layout": ([_I32], _I32),
     "p2p_delta_snapshot_f32": ([_P, _P, _P, _I64, _I32, _P], _I32),
     "p2p_delta_snapshot_segments_f32": ([_P, _I32, _I64, _I32, _P], _I32),
 }

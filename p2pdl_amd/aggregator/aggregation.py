@@ -80,7 +80,12 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
                 raise RuntimeError(f"update {j} key {key}: {tuple(u.shape)} does not match "
                                    f"{tuple(w.shape)}")
             if u.dtype != torch.float32:
-                u = u.to(torch.float32)
+                if u.dtype == torch.float64 or u.is_complex():
+                    # the reference's in-place `acc += u` (:28) adds in float64 and rounds
+                    # once; casting u to fp32 first would round twice (1-ulp differences)
+                    raise TypeError(f"update {j} key {key} is {u.dtype}; p2pdl_amd aggregates float32 "
+                                    f"updates (fp16 / bf16 / integer updates are widened exactly)")
+                u = u.to(torch.float32)  # exact widening: what the reference's add computes in
             row.append(u.contiguous())
         peer_lists.append(row)
 

@@ -112,31 +112,12 @@ extern "C" int32_t p2p_delta_snapshot_f32(const float* cur, float* prev, float* 
       3)
     return P2P_ERR_ALIGN;
   if (n == 0) return P2P_OK;
-  // Tuning knobs (measured in DESIGN.md): floats per lane per tensor (NV x 4)
-  // and nontemporal vs plain stores.
-  static const int nv = [] {
-    const char* e = getenv("P2P_DELTA_NV");
-    const int v = e ? atoi(e) : kDNV;
-    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : kDNV;
-  }();
-  static const bool nt = [] {
-    const char* e = getenv("P2P_DELTA_NT");
-    return !(e && atoi(e) == 0);
-  }();
-  const int64_t tiles = ceil_div(n, static_cast<int64_t>(kBlock) * 4 * nv);
-  hipStream_t s = static_cast<hipStream_t>(stream);
+  // 4 float4 per lane per tensor with nontemporal stores: the fastest of the
+  // NV in {1, 2, 4, 8} x {plain, nontemporal} grid measured.
+  const int64_t tiles = ceil_div(n, kDTile);
   if (tiles > 0x7FFFFFFFll) return P2P_ERR_UNSUPPORTED;
-  const dim3 g(static_cast<unsigned>(tiles)), b(kBlock);
-#define P2P_DLAUNCH(NV_)                                                                              \
-  if (nt) hipLaunchKernelGGL((delta_flat_kernel<NV_, true>), g, b, 0, s, cur, prev, delta, n, first); \
-  else hipLaunchKernelGGL((delta_flat_kernel<NV_, false>), g, b, 0, s, cur, prev, delta, n, first)
-  switch (nv) {
-    case 1: P2P_DLAUNCH(1); break;
-    case 2: P2P_DLAUNCH(2); break;
-    case 8: P2P_DLAUNCH(8); break;
-    default: P2P_DLAUNCH(4); break;
-  }
-#undef P2P_DLAUNCH
+  hipLaunchKernelGGL((delta_flat_kernel<kDNV, true>), dim3(static_cast<unsigned>(tiles)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), cur, prev, delta, n, first);
   return delta_status();
 }
 

@@ -19,16 +19,20 @@
 // nontemporal loads (read once), one tile per block.  128 GB cfg3 tile:
 // 6.2-6.4 TB/s = 78-80% of 8 TB/s.  No inter-block reuse exists, so no XCD
 // remap is needed (guide T1: 0% on elementwise).
-#include <stdlib.h>
-
 #include "p2p_common.h"
 
 namespace p2p {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kNV = 4;                    // float4s per lane per tile (segment kernel)
-constexpr int kTile = kBlock * 4 * kNV;   // 4096 floats per tile
+// One float4 per lane per peer per tile (1024 floats, 56 VGPRs, full
+// occupancy) for flat buffers AND state_dict segments.  Measured against
+// 4096-float tiles: cfg2 (64 x 11.7M) 76.8% vs 71.4% of HBM peak -- 2854
+// tiles of 4096 leave the last wave of blocks part-empty, and the 4-float4
+// segment kernel needed 150 VGPRs (occupancy 3) -- and cfg3 (256 x 125M)
+// 77.9% vs 77.1%.
+constexpr int kNV = 1;
+constexpr int kTile = kBlock * 4 * kNV;   // 1024 floats per tile
 template <int NV> constexpr int tile_of() { return kBlock * 4 * NV; }
 constexpr int kUnroll = 8;
 
@@ -172,36 +176,10 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* ag
 
 static int grid_for_tiles(int64_t ntiles) { return static_cast<int>(ntiles > 0 ? ntiles : 1); }
 
-// Flat launches use 1024-float tiles (one float4 per lane per peer, 8 peers
-// of loads in flight, 56 VGPRs -> full occupancy).  Measured against 4096:
-// cfg2 (64 x 11.7M) 76.8% vs 71.4% of HBM peak -- 2854 tiles of 4096 leave
-// the last wave of blocks part-empty -- and cfg3 (256 x 125M) 77.9% vs
-// 77.1%.  P2P_FEDAVG_NV forces 1, 2 or 4 (A/B).
-static int flat_nv(int64_t n) {
-  static const int forced = [] {
-    const char* e = getenv("P2P_FEDAVG_NV");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced == 1 || forced == 2 || forced == 4) return forced;
-  (void)n;
-  return 1;
-}
-
 static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,
                         float lr, hipStream_t stream) {
-  switch (flat_nv(n)) {
-    case 1:
-      hipLaunchKernelGGL(fedavg_flat_kernel<1>, dim3(grid_for_tiles(ceil_div(n, tile_of<1>()))), dim3(kBlock), 0,
-                         stream, peers, K, k_dev, n, w, out, lr);
-      break;
-    case 2:
-      hipLaunchKernelGGL(fedavg_flat_kernel<2>, dim3(grid_for_tiles(ceil_div(n, tile_of<2>()))), dim3(kBlock), 0,
-                         stream, peers, K, k_dev, n, w, out, lr);
-      break;
-    default:
-      hipLaunchKernelGGL(fedavg_flat_kernel<4>, dim3(grid_for_tiles(ceil_div(n, tile_of<4>()))), dim3(kBlock), 0,
-                         stream, peers, K, k_dev, n, w, out, lr);
-  }
+  hipLaunchKernelGGL(fedavg_flat_kernel<kNV>, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0, stream,
+                     peers, K, k_dev, n, w, out, lr);
 }
 
 static int grid_stride_blocks(int64_t nblocks) {

@@ -610,31 +610,21 @@ static void launch_lds(const LdsArgs& a) {
 
 using namespace p2p;
 
-// Layout for K (p2p_robust_lds_tile and the launch must agree): K in 129..256
-// -> 4 lanes x 64 keys; K in 65..128 -> 4 lanes x 32 keys (variant 0), 2
-// lanes x 64 keys (1) or one lane x 128 keys (2) (tuning knob, robust.hip).
-extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t k, int32_t variant) {
-  if (variant == 3) return LdsLayout<4, 64, 0, 2>::TB;  // radix16 (median, K = 256 only)
-  if (k > 128) return LdsLayout<4, 64>::TB;
-  return variant == 1 ? LdsLayout<2, 64>::TB : variant == 2 ? LdsLayout<1, 128>::TB : LdsLayout<4, 32>::TB;
+// K in 129..256: 4 lanes x 64 keys per coordinate (p2p_robust_lds_tile and the
+// launch must agree; the tile size is a pure function of (rule, k)).  Other
+// instantiations of the templates above (4 x 32, 2 x 64, 1 x 128, radix16)
+// are built only into the A/B library of tools/robust_lab.hip.
+extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t rule, int32_t k) {
+  (void)rule;
+  (void)k;
+  return LdsLayout<4, 64>::TB;
 }
 
 extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, const p2p_segment_t* segs,
                                                    int32_t nseg, int64_t tiles, int32_t k, int32_t rule,
                                                    int32_t trim_b, int64_t n, float* w, float* out, float lr,
-                                                   int32_t variant, p2p_stream_t stream) {
+                                                   p2p_stream_t stream) {
   LdsArgs a{peers, segs, nseg, tiles, k, trim_b, n, w, out, lr, static_cast<hipStream_t>(stream)};
-  const bool med = rule == P2P_RULE_MEDIAN;
-  if (variant == 3) {  // radix16: the caller routes only median at K = 256 here
-    if (segs) launch_lds_kernel<4, 64, P2P_RULE_MEDIAN, 1, true, 0, 2>(a);
-    else launch_lds_kernel<4, 64, P2P_RULE_MEDIAN, 1, false, 0, 2>(a);
-  } else if (k > 128) {
-    if (med) launch_lds<4, 64, P2P_RULE_MEDIAN>(a); else launch_lds<4, 64, P2P_RULE_TRIMMED>(a);
-  } else if (variant == 1) {
-    if (med) launch_lds<2, 64, P2P_RULE_MEDIAN>(a); else launch_lds<2, 64, P2P_RULE_TRIMMED>(a);
-  } else if (variant == 2) {
-    if (med) launch_lds<1, 128, P2P_RULE_MEDIAN>(a); else launch_lds<1, 128, P2P_RULE_TRIMMED>(a);
-  } else {
-    if (med) launch_lds<4, 32, P2P_RULE_MEDIAN>(a); else launch_lds<4, 32, P2P_RULE_TRIMMED>(a);
-  }
+  if (rule == P2P_RULE_MEDIAN) launch_lds<4, 64, P2P_RULE_MEDIAN>(a);
+  else launch_lds<4, 64, P2P_RULE_TRIMMED>(a);
 }

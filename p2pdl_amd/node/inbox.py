@@ -12,14 +12,16 @@ Here:
   * ``recv_message`` reads the 4-byte length and ``recv_into`` one
     preallocated buffer (linear);
   * ``ZeroCopyParser`` decodes the serialized update WITHOUT executing it: a
-    restricted stack machine over the opcodes torch emits (protocols 3-5)
+    restricted stack machine over the opcodes torch emits (protocols 2-5)
     that resolves only the tensor-rebuild / legacy-storage callables and
-    OrderedDict, parses the legacy storage blobs itself (magic, header
-    pickles, raw little-endian payload) and hands the payloads out as
-    memoryview slices of the message -- no copy.  Anything else in the stream
-    raises ``pickle.UnpicklingError`` -- unlike the reference's
-    ``pickle.loads`` on network bytes.  (``UpdateParser`` is the same
-    restriction on top of the C unpickler, which copies each payload once.)
+    OrderedDict, parses the legacy storage blobs with the same machine
+    (magic, header pickles, raw little-endian payload), checks every tensor
+    view against its storage, and hands the payloads out as memoryview
+    slices of the message -- no copy.  Anything else in the stream, and any
+    malformed byte, raises ``pickle.UnpicklingError`` -- unlike the
+    reference's ``pickle.loads`` on network bytes.  The stdlib unpickler is
+    never run on peer bytes (its memo array lets a LONG_BINPUT index
+    allocate gigabytes).
   * ``DeviceInbox.land`` copies the fp32 tensors of one update into row k of a
     preallocated [K_max, N] fp32 slab on the GPU through a pinned staging row
     -- one host-to-device copy per update -- and returns a state_dict whose
@@ -34,6 +36,7 @@ from __future__ import annotations
 import os
 import pickle
 import struct
+import threading
 from collections import OrderedDict
 from dataclasses import dataclass
 
@@ -84,77 +87,259 @@ class RawTensor:
                                                strides=tuple(s * item for s in self.stride), writeable=False)
 
 
-class _Reader:
-    """Minimal read-only file over a buffer: pickle pulls only what it parses
-    (io.BytesIO would first copy the whole message)."""
-
-    def __init__(self, buf):
-        self.mv = memoryview(buf).cast("B")
-        self.pos = 0
-
-    def read(self, n=-1):
-        end = len(self.mv) if n is None or n < 0 else min(len(self.mv), self.pos + n)
-        out = self.mv[self.pos:end].tobytes()
-        self.pos = end
-        return out
-
-    def readinto(self, b):
-        n = min(len(b), len(self.mv) - self.pos)
-        b[:n] = self.mv[self.pos:self.pos + n]
-        self.pos += n
-        return n
-
-    def readline(self):
-        end = self.pos
-        while end < len(self.mv):
-            chunk = self.mv[end:end + 256].tobytes()
-            i = chunk.find(b"\n")
-            if i >= 0:
-                end += i + 1
-                break
-            end += len(chunk)
-        return self.read(end - self.pos)
-
-    def tell(self):
-        return self.pos
+class _Mark:
+    pass
 
 
-class _StorageHeader(pickle.Unpickler):
-    """Unpickles the header pickles of one legacy storage blob."""
+_MARK = _Mark()
 
-    def find_class(self, module, name):
-        if module == "torch" and name in _STORAGE_DTYPES:
-            return name  # the storage type, as its name
-        raise pickle.UnpicklingError(f"unexpected global {module}.{name} in a tensor storage blob")
+# what malformed bytes make the stack machine raise (converted to
+# pickle.UnpicklingError at the parser boundary)
+_MALFORMED = (KeyError, IndexError, ValueError, TypeError, AttributeError, UnicodeDecodeError,
+              struct.error, RecursionError, OverflowError, MemoryError)
 
-    def persistent_load(self, pid):
-        if not (isinstance(pid, tuple) and len(pid) >= 5 and pid[0] == "storage"):
-            raise pickle.UnpicklingError(f"unexpected persistent id {pid!r}")
-        self.pid = pid
-        return pid
+
+def _run_pickle(mv: memoryview, pos: int, *, min_proto: int, resolve_global, persistent_load=None):
+    """Restricted pickle stack machine over mv[pos:]: runs ONE pickle up to
+    its STOP and returns (object, position after STOP).
+
+    Only the opcodes torch emits for a state_dict and for the header pickles
+    of a legacy storage blob (protocols 2-5) are accepted.  Globals resolve
+    through ``resolve_global(module, name)`` (an allow-list); REDUCE calls
+    only what that returned.  Byte strings come back as memoryview slices of
+    mv (no copy).  The memo is a dict (a LONG_BINPUT with a huge index costs
+    nothing, unlike the C unpickler's memo array) and every length field is
+    checked against the end of the buffer."""
+    n = len(mv)
+    stack: list = []
+    memo: dict = {}
+
+    def need(p, k):  # bytes [p, p+k) must exist
+        if k < 0 or p + k > n:
+            raise pickle.UnpicklingError("truncated pickle")
+
+    def le(p, k):
+        need(p, k)
+        return int.from_bytes(mv[p:p + k], "little")
+
+    def blob(p, k):
+        need(p, k)
+        return mv[p:p + k]
+
+    def pop_mark():
+        nonlocal stack
+        for i in range(len(stack) - 1, -1, -1):
+            if stack[i] is _MARK:
+                items = stack[i + 1:]
+                stack = stack[:i]
+                return items
+        raise pickle.UnpicklingError("MARK not found")
+
+    while pos < n:
+        op = mv[pos]
+        pos += 1
+        if op == 0x80:            # PROTO
+            if le(pos, 1) < min_proto:
+                raise pickle.UnpicklingError(f"pickle protocol {mv[pos]} (< {min_proto}) is not accepted")
+            pos += 1
+        elif op == 0x95:          # FRAME (8-byte length; frames are inline)
+            need(pos, 8)
+            pos += 8
+        elif op == 0x2E:          # STOP
+            return stack.pop(), pos
+        elif op == 0x28:          # MARK
+            stack.append(_MARK)
+        elif op == 0x7D:          # EMPTY_DICT
+            stack.append({})
+        elif op == 0x29:          # EMPTY_TUPLE
+            stack.append(())
+        elif op == 0x5D:          # EMPTY_LIST
+            stack.append([])
+        elif op == 0x94:          # MEMOIZE
+            memo[len(memo)] = stack[-1]
+        elif op == 0x71:          # BINPUT
+            memo[le(pos, 1)] = stack[-1]
+            pos += 1
+        elif op == 0x72:          # LONG_BINPUT
+            memo[le(pos, 4)] = stack[-1]
+            pos += 4
+        elif op == 0x68:          # BINGET
+            stack.append(memo[le(pos, 1)])
+            pos += 1
+        elif op == 0x6A:          # LONG_BINGET
+            stack.append(memo[le(pos, 4)])
+            pos += 4
+        elif op == 0x8C:          # SHORT_BINUNICODE
+            k = le(pos, 1)
+            stack.append(str(blob(pos + 1, k), "utf-8"))
+            pos += 1 + k
+        elif op == 0x58:          # BINUNICODE
+            k = le(pos, 4)
+            stack.append(str(blob(pos + 4, k), "utf-8"))
+            pos += 4 + k
+        elif op == 0x43:          # SHORT_BINBYTES
+            k = le(pos, 1)
+            stack.append(blob(pos + 1, k))
+            pos += 1 + k
+        elif op == 0x42:          # BINBYTES
+            k = le(pos, 4)
+            stack.append(blob(pos + 4, k))
+            pos += 4 + k
+        elif op == 0x8E:          # BINBYTES8
+            k = le(pos, 8)
+            stack.append(blob(pos + 8, k))
+            pos += 8 + k
+        elif op == 0x4B:          # BININT1
+            stack.append(le(pos, 1))
+            pos += 1
+        elif op == 0x4D:          # BININT2
+            stack.append(le(pos, 2))
+            pos += 2
+        elif op == 0x4A:          # BININT (signed)
+            stack.append(int.from_bytes(blob(pos, 4), "little", signed=True))
+            pos += 4
+        elif op == 0x8A:          # LONG1
+            k = le(pos, 1)
+            stack.append(int.from_bytes(blob(pos + 1, k), "little", signed=True))
+            pos += 1 + k
+        elif op == 0x89:          # NEWFALSE
+            stack.append(False)
+        elif op == 0x88:          # NEWTRUE
+            stack.append(True)
+        elif op == 0x4E:          # NONE
+            stack.append(None)
+        elif op == 0x85:          # TUPLE1
+            stack[-1] = (stack[-1],)
+        elif op == 0x86:          # TUPLE2
+            b = stack.pop()
+            stack[-1] = (stack[-1], b)
+        elif op == 0x87:          # TUPLE3
+            c = stack.pop()
+            b = stack.pop()
+            stack[-1] = (stack[-1], b, c)
+        elif op == 0x74:          # TUPLE
+            items = pop_mark()  # rebinds `stack`: take the items first
+            stack.append(tuple(items))
+        elif op == 0x93:          # STACK_GLOBAL
+            name = stack.pop()
+            module = stack.pop()
+            if not (isinstance(module, str) and isinstance(name, str)):
+                raise pickle.UnpicklingError("STACK_GLOBAL needs two strings")
+            stack.append(resolve_global(module, name))
+        elif op == 0x63:          # GLOBAL (text: module\nname\n)
+            e1 = bytes(mv[pos:pos + 256]).index(b"\n")
+            module = str(mv[pos:pos + e1], "ascii")
+            e2 = bytes(mv[pos + e1 + 1:pos + e1 + 257]).index(b"\n")
+            name = str(mv[pos + e1 + 1:pos + e1 + 1 + e2], "ascii")
+            pos += e1 + e2 + 2
+            stack.append(resolve_global(module, name))
+        elif op == 0x51:          # BINPERSID
+            if persistent_load is None:
+                raise pickle.UnpicklingError("persistent ids are not accepted here")
+            stack[-1] = persistent_load(stack[-1])
+        elif op == 0x52:          # REDUCE
+            args = stack.pop()
+            fn = stack[-1]
+            if not isinstance(fn, _Callable) or not isinstance(args, tuple):
+                raise pickle.UnpicklingError("REDUCE of something that is not an allowed global")
+            stack[-1] = fn(*args)
+        elif op == 0x62:          # BUILD (OrderedDict metadata: set attributes)
+            state = stack.pop()
+            inst = stack[-1]
+            if isinstance(state, dict) and isinstance(inst, OrderedDict):
+                # torch sets only `_metadata`; any other attribute could
+                # shadow the dict's methods (items / values) on the instance
+                if set(state) - {"_metadata"}:
+                    raise pickle.UnpicklingError("unexpected attributes on a state_dict")
+                inst.__dict__.update(state)
+            elif state is not None:
+                raise pickle.UnpicklingError("unexpected BUILD")
+        elif op == 0x73:          # SETITEM
+            v = stack.pop()
+            k = stack.pop()
+            dict.__setitem__(stack[-1], k, v)
+        elif op == 0x75:          # SETITEMS
+            items = pop_mark()
+            d = stack[-1]
+            for i in range(0, len(items), 2):
+                dict.__setitem__(d, items[i], items[i + 1])
+        elif op == 0x61:          # APPEND
+            v = stack.pop()
+            list.append(stack[-1], v)
+        elif op == 0x65:          # APPENDS
+            items = pop_mark()
+            list.extend(stack[-1], items)
+        else:
+            raise pickle.UnpicklingError(f"opcode 0x{op:02x} is not accepted in a peer update")
+    raise pickle.UnpicklingError("truncated pickle")
+
+
+class _Callable:
+    """An allow-listed global (the only thing REDUCE may call)."""
+
+    def __init__(self, fn, name):
+        self.fn, self.name = fn, name
+
+    def __call__(self, *args):
+        return self.fn(*args)
+
+
+class _StorageType(str):
+    """A torch.<X>Storage global of a storage record, kept as its name."""
+
+
+def _storage_global(module, name):
+    if module == "torch" and name in _STORAGE_DTYPES:
+        return _StorageType(name)
+    raise pickle.UnpicklingError(f"unexpected global {module}.{name} in a tensor storage blob")
+
+
+def _no_global(module, name):
+    raise pickle.UnpicklingError(f"unexpected global {module}.{name} in a tensor storage header")
 
 
 def parse_legacy_storage(blob) -> RawStorage:
+    """One torch legacy storage blob (torch/serialization.py _legacy_save): the
+    magic-number, protocol-version and sys_info pickles (no globals allowed),
+    the storage record (a persistent id naming the storage type, key,
+    location and element count), the key-list pickle, then an int64 count
+    and the raw little-endian payload.  Every pickle runs on the restricted
+    machine: the blob is the peer's."""
+    if not isinstance(blob, (memoryview, bytes, bytearray)):
+        raise pickle.UnpicklingError("storage blob must be bytes")
     mv = memoryview(blob).cast("B")
-    f = _Reader(mv)
-    if pickle.Unpickler(f).load() != _LEGACY_MAGIC:
+    magic, pos = _run_pickle(mv, 0, min_proto=2, resolve_global=_no_global)
+    if type(magic) is not int or magic != _LEGACY_MAGIC:
         raise pickle.UnpicklingError("not a torch legacy storage blob (magic)")
-    f_ver = pickle.Unpickler(f).load()
-    if f_ver != 1001:
-        raise pickle.UnpicklingError(f"unsupported legacy protocol version {f_ver}")
-    pickle.Unpickler(f).load()  # sys_info
-    hdr = _StorageHeader(f)
-    hdr.load()
-    _, stype, key, location, numel = hdr.pid[:5]
-    if len(hdr.pid) > 5 and hdr.pid[5] is not None:
+    f_ver, pos = _run_pickle(mv, pos, min_proto=2, resolve_global=_no_global)
+    if type(f_ver) is not int or f_ver != 1001:
+        raise pickle.UnpicklingError(f"unsupported legacy protocol version {f_ver!r}")
+    sys_info, pos = _run_pickle(mv, pos, min_proto=2, resolve_global=_no_global)
+    if not isinstance(sys_info, dict) or sys_info.get("little_endian") is not True:
+        raise pickle.UnpicklingError("storage blob is not little-endian")
+    pids = []
+
+    def persistent_load(pid):
+        pids.append(pid)
+        return None
+
+    _, pos = _run_pickle(mv, pos, min_proto=2, resolve_global=_storage_global, persistent_load=persistent_load)
+    if len(pids) != 1 or not isinstance(pids[0], tuple) or len(pids[0]) < 5 or pids[0][0] != "storage":
+        raise pickle.UnpicklingError("storage blob without exactly one storage record")
+    pid = pids[0]
+    _, stype, key, location, numel = pid[:5]
+    if not isinstance(stype, _StorageType) or type(numel) is not int or numel < 0 or not isinstance(key, str):
+        raise pickle.UnpicklingError("malformed storage record")
+    if len(pid) > 5 and pid[5] is not None:
         raise pickle.UnpicklingError("storage views are not supported")
-    keys = _StorageHeader(f).load()
+    keys, pos = _run_pickle(mv, pos, min_proto=2, resolve_global=_no_global)
     if keys != [key]:
         raise pickle.UnpicklingError("expected exactly one storage per blob")
     dt = _STORAGE_DTYPES[stype]
     if dt is None:
         raise pickle.UnpicklingError(f"{stype} is not supported")
-    pos = f.tell()
+    if pos + 8 > len(mv):
+        raise pickle.UnpicklingError("truncated storage blob")
     (count,) = struct.unpack_from("<q", mv, pos)
     nbytes = count * np.dtype(dt).itemsize
     if count != numel or pos + 8 + nbytes != len(mv):
@@ -162,205 +347,81 @@ def parse_legacy_storage(blob) -> RawStorage:
     return RawStorage(dt, int(numel), mv[pos + 8:pos + 8 + nbytes], str(location))
 
 
+def _is_index(x) -> bool:
+    return type(x) is int and x >= 0
+
+
 def _rebuild_tensor_v2(storage, offset, size, stride, requires_grad=False, hooks=None, metadata=None):
+    """The view a peer claims must lie inside its storage (torch's own
+    set_() refuses it otherwise): non-negative integer offset, sizes and
+    strides, and the last addressed element below storage.numel.  Without
+    this an as_strided view would read past the message buffer."""
     if not isinstance(storage, RawStorage):
         raise pickle.UnpicklingError("tensor without a storage")
-    return RawTensor(storage, int(offset), tuple(size), tuple(stride))
+    if not (isinstance(size, tuple) and isinstance(stride, tuple) and len(size) == len(stride)):
+        raise pickle.UnpicklingError("tensor size / stride must be tuples of the same length")
+    if not (_is_index(offset) and all(map(_is_index, size)) and all(map(_is_index, stride))):
+        raise pickle.UnpicklingError("tensor offset, sizes and strides must be non-negative integers")
+    if all(size):  # non-empty: the furthest element must exist
+        last = offset + sum((s - 1) * st for s, st in zip(size, stride))
+        if last >= storage.numel:
+            raise pickle.UnpicklingError(f"tensor view ends at element {last}, storage holds {storage.numel}")
+    elif offset > storage.numel:
+        raise pickle.UnpicklingError("tensor offset past the end of its storage")
+    return RawTensor(storage, offset, size, stride)
 
 
-class UpdateParser(pickle.Unpickler):
-    """Restricted unpickler for a pickled state_dict (reference node/node.py:285)."""
-
-    _ALLOWED = {
-        ("torch._utils", "_rebuild_tensor_v2"): _rebuild_tensor_v2,
-        ("torch.storage", "_load_from_bytes"): parse_legacy_storage,
-        ("collections", "OrderedDict"): OrderedDict,
-    }
-
-    def find_class(self, module, name):
-        fn = self._ALLOWED.get((module, name))
-        if fn is None:
-            raise pickle.UnpicklingError(f"refusing to load global {module}.{name} from a peer update")
-        return fn
-
-    @classmethod
-    def parse(cls, data) -> dict:
-        obj = cls(_Reader(data)).load()
-        if not isinstance(obj, dict) or not all(isinstance(v, RawTensor) for v in obj.values()):
-            raise pickle.UnpicklingError("a peer update must be a dict of tensors")
-        return obj
+def _ordered_dict(*args):
+    if args:
+        raise pickle.UnpicklingError("OrderedDict with arguments")
+    return OrderedDict()
 
 
-class _Mark:
-    pass
+# The globals a pickled state_dict of tensors needs (torch's tensor pickling:
+# _rebuild_tensor_v2 over a legacy-format storage blob; the OrderedDict of
+# state_dict()).  Nothing else resolves.
+_UPDATE_GLOBALS = {
+    ("torch._utils", "_rebuild_tensor_v2"): _Callable(_rebuild_tensor_v2, "_rebuild_tensor_v2"),
+    ("torch.storage", "_load_from_bytes"): _Callable(parse_legacy_storage, "_load_from_bytes"),
+    ("collections", "OrderedDict"): _Callable(_ordered_dict, "OrderedDict"),
+}
 
 
-_MARK = _Mark()
+def _update_global(module, name):
+    fn = _UPDATE_GLOBALS.get((module, name))
+    if fn is None:
+        raise pickle.UnpicklingError(f"refusing to load global {module}.{name} from a peer update")
+    return fn
+
+
+def _is_tensor_dict(obj) -> bool:
+    """A dict whose values are all tensors (dict.values, not obj.values: the
+    method lookup must not go through attributes a pickle could set)."""
+    return isinstance(obj, dict) and all(isinstance(v, RawTensor) for v in dict.values(obj))
 
 
 class ZeroCopyParser:
-    """Restricted stack-machine reader for the pickled state_dict of a peer
-    update (pickle protocols 3-5, the opcodes torch emits for a dict of
-    tensors).  Byte strings are returned as memoryview slices of the message
-    buffer -- the tensor payloads are never copied by the parser -- and only
-    the globals of ``UpdateParser`` resolve; anything else raises
-    ``pickle.UnpicklingError``."""
+    """Reader for the pickled state_dict of a peer update (reference
+    node/node.py:285; pickle protocols 3-5).  Runs the restricted stack
+    machine: byte strings are memoryview slices of the message buffer -- the
+    tensor payloads are never copied -- only the three globals above resolve,
+    and anything else, or any malformed byte, raises
+    ``pickle.UnpicklingError`` (so a listener that catches only that cannot
+    be killed by a peer's bytes)."""
 
     def __init__(self, data):
         self.mv = memoryview(data).cast("B")
 
     def parse(self) -> dict:
-        mv = self.mv
-        n = len(mv)
-        pos = 0
-        stack: list = []
-        memo: dict = {}
-        u8 = lambda p: mv[p]  # noqa: E731
-        le = lambda p, k: int.from_bytes(mv[p:p + k], "little")  # noqa: E731
-
-        def pop_mark():
-            nonlocal stack
-            for i in range(len(stack) - 1, -1, -1):
-                if stack[i] is _MARK:
-                    items = stack[i + 1:]
-                    stack = stack[:i]
-                    return items
-            raise pickle.UnpicklingError("MARK not found")
-
-        while pos < n:
-            op = mv[pos]
-            pos += 1
-            if op == 0x80:            # PROTO
-                if mv[pos] < 3:
-                    raise pickle.UnpicklingError(f"pickle protocol {mv[pos]} (< 3) is not accepted")
-                pos += 1
-            elif op == 0x95:          # FRAME (8-byte length; frames are inline)
-                pos += 8
-            elif op == 0x2E:          # STOP
-                result = stack.pop()
-                if not isinstance(result, dict) or not all(isinstance(v, RawTensor) for v in result.values()):
-                    raise pickle.UnpicklingError("a peer update must be a dict of tensors")
-                return result
-            elif op == 0x28:          # MARK
-                stack.append(_MARK)
-            elif op == 0x7D:          # EMPTY_DICT
-                stack.append({})
-            elif op == 0x29:          # EMPTY_TUPLE
-                stack.append(())
-            elif op == 0x5D:          # EMPTY_LIST
-                stack.append([])
-            elif op == 0x94:          # MEMOIZE
-                memo[len(memo)] = stack[-1]
-            elif op == 0x71:          # BINPUT
-                memo[mv[pos]] = stack[-1]
-                pos += 1
-            elif op == 0x72:          # LONG_BINPUT
-                memo[le(pos, 4)] = stack[-1]
-                pos += 4
-            elif op == 0x68:          # BINGET
-                stack.append(memo[mv[pos]])
-                pos += 1
-            elif op == 0x6A:          # LONG_BINGET
-                stack.append(memo[le(pos, 4)])
-                pos += 4
-            elif op == 0x8C:          # SHORT_BINUNICODE
-                k = mv[pos]
-                stack.append(str(mv[pos + 1:pos + 1 + k], "utf-8"))
-                pos += 1 + k
-            elif op == 0x58:          # BINUNICODE
-                k = le(pos, 4)
-                stack.append(str(mv[pos + 4:pos + 4 + k], "utf-8"))
-                pos += 4 + k
-            elif op == 0x43:          # SHORT_BINBYTES
-                k = mv[pos]
-                stack.append(mv[pos + 1:pos + 1 + k])
-                pos += 1 + k
-            elif op == 0x42:          # BINBYTES
-                k = le(pos, 4)
-                stack.append(mv[pos + 4:pos + 4 + k])
-                pos += 4 + k
-            elif op == 0x8E:          # BINBYTES8
-                k = le(pos, 8)
-                stack.append(mv[pos + 8:pos + 8 + k])
-                pos += 8 + k
-            elif op == 0x4B:          # BININT1
-                stack.append(mv[pos])
-                pos += 1
-            elif op == 0x4D:          # BININT2
-                stack.append(le(pos, 2))
-                pos += 2
-            elif op == 0x4A:          # BININT (signed)
-                stack.append(int.from_bytes(mv[pos:pos + 4], "little", signed=True))
-                pos += 4
-            elif op == 0x8A:          # LONG1
-                k = mv[pos]
-                stack.append(int.from_bytes(mv[pos + 1:pos + 1 + k], "little", signed=True))
-                pos += 1 + k
-            elif op == 0x89:          # NEWFALSE
-                stack.append(False)
-            elif op == 0x88:          # NEWTRUE
-                stack.append(True)
-            elif op == 0x4E:          # NONE
-                stack.append(None)
-            elif op == 0x85:          # TUPLE1
-                stack[-1] = (stack[-1],)
-            elif op == 0x86:          # TUPLE2
-                b = stack.pop()
-                stack[-1] = (stack[-1], b)
-            elif op == 0x87:          # TUPLE3
-                c = stack.pop()
-                b = stack.pop()
-                stack[-1] = (stack[-1], b, c)
-            elif op == 0x74:          # TUPLE
-                items = pop_mark()  # rebinds `stack`: take the items first
-                stack.append(tuple(items))
-            elif op == 0x93:          # STACK_GLOBAL
-                name = stack.pop()
-                module = stack.pop()
-                stack.append(self._global(module, name))
-            elif op == 0x63:          # GLOBAL (text: module\nname\n)
-                e1 = bytes(mv[pos:pos + 256]).index(b"\n")
-                module = str(mv[pos:pos + e1], "ascii")
-                e2 = bytes(mv[pos + e1 + 1:pos + e1 + 257]).index(b"\n")
-                name = str(mv[pos + e1 + 1:pos + e1 + 1 + e2], "ascii")
-                pos += e1 + e2 + 2
-                stack.append(self._global(module, name))
-            elif op == 0x52:          # REDUCE
-                args = stack.pop()
-                fn = stack[-1]
-                stack[-1] = fn(*args)
-            elif op == 0x62:          # BUILD (OrderedDict metadata: set attributes)
-                state = stack.pop()
-                inst = stack[-1]
-                if isinstance(state, dict) and isinstance(inst, OrderedDict):
-                    inst.__dict__.update({k: v for k, v in state.items() if isinstance(k, str)})
-                elif state is not None:
-                    raise pickle.UnpicklingError("unexpected BUILD")
-            elif op == 0x73:          # SETITEM
-                v = stack.pop()
-                k = stack.pop()
-                stack[-1][k] = v
-            elif op == 0x75:          # SETITEMS
-                items = pop_mark()
-                d = stack[-1]
-                for i in range(0, len(items), 2):
-                    d[items[i]] = items[i + 1]
-            elif op == 0x61:          # APPEND
-                v = stack.pop()
-                stack[-1].append(v)
-            elif op == 0x65:          # APPENDS
-                items = pop_mark()
-                stack[-1].extend(items)
-            else:
-                raise pickle.UnpicklingError(f"opcode 0x{op:02x} is not accepted in a peer update")
-        raise pickle.UnpicklingError("truncated pickle")
-
-    @staticmethod
-    def _global(module, name):
-        fn = UpdateParser._ALLOWED.get((module, name))
-        if fn is None:
-            raise pickle.UnpicklingError(f"refusing to load global {module}.{name} from a peer update")
-        return fn
+        try:
+            obj, _ = _run_pickle(self.mv, 0, min_proto=3, resolve_global=_update_global)
+        except pickle.UnpicklingError:
+            raise
+        except _MALFORMED as e:
+            raise pickle.UnpicklingError(f"malformed peer update: {type(e).__name__}: {e}") from e
+        if not _is_tensor_dict(obj):
+            raise pickle.UnpicklingError("a peer update must be a dict of tensors")
+        return OrderedDict(dict.items(obj))  # a fresh dict: no attributes the pickle set
 
 
 def recv_exact_into(conn, buf: memoryview) -> int:
@@ -413,9 +474,14 @@ class DeviceInbox:
         self._stage = [torch.empty(self.row, dtype=torch.float32, pin_memory=True) for _ in range(2)]
         self._events = [None, None]
         self.count = 0
+        # land() is called from the listener threads (one per connection,
+        # reference node/node.py:89): row reservation and the staging ->
+        # device sequence are serialised; parsing runs outside the lock.
+        self._lock = threading.Lock()
 
     def reset(self) -> None:
-        self.count = 0
+        with self._lock:
+            self.count = 0
 
     def land(self, serialized, k: int | None = None) -> dict:
         """Parse one serialized update and copy it to slab row k (next free row
@@ -424,11 +490,15 @@ class DeviceInbox:
         The payloads go message buffer -> pinned staging row (one memcpy,
         split across a thread pool) -> device (one DMA)."""
         raw = ZeroCopyParser(serialized).parse()
-        if k is None:
-            k = self.count
-        if not 0 <= k < self.k_max:
-            raise IndexError(f"slab row {k} out of range (k_max={self.k_max})")
-        self.count = max(self.count, k + 1)
+        with self._lock:
+            if k is None:
+                k = self.count
+            if not 0 <= k < self.k_max:
+                raise IndexError(f"slab row {k} out of range (k_max={self.k_max})")
+            self.count = max(self.count, k + 1)
+            return self._land_locked(raw, k)
+
+    def _land_locked(self, raw, k: int) -> dict:
         s = k & 1
         if self._events[s] is not None:
             self._events[s].synchronize()  # the staging row is free again
@@ -436,7 +506,7 @@ class DeviceInbox:
         row = self.slab[k]
         out = OrderedDict()
         jobs = []
-        for key, rt in raw.items():
+        for key, rt in dict.items(raw):
             lay = self.layout.get(key)
             if lay is not None and rt.storage.dtype is np.float32:
                 off, shape, n = lay

@@ -319,18 +319,3 @@ def fill_synthetic_(out: torch.Tensor, seed: int, peer: int, scale: float, chunk
                                                chunk, nranks, rank, N.stream_handle()),
                 "p2p_fill_synthetic_f32")
     return out
-
-
-ROBUST_LAYOUTS = {"auto": 0, "lds": 1, "lds2": 2, "group": 3, "lds1": 4, "radix16": 5}
-
-
-def set_robust_layout(layout: str | int) -> None:
-    """Tuning knob (process-wide): kernel layout for robust rules at K in 65..256.
-
-    "auto" (default): fastest measured per K; "lds": 4 lanes per coordinate,
-    peer rows LDS-DMA staged; "lds2": 2 lanes x 64 keys for K <= 128;
-    "lds1": one lane x 128 keys, LDS-DMA staged, for K <= 128;
-    "group": the one-lane / wave-group kernels.  All give identical results; tables for aggregate_segments_ must
-    be built after the layout is chosen (their tile size depends on it)."""
-    code = ROBUST_LAYOUTS[layout] if isinstance(layout, str) else int(layout)
-    N.check(N.lib().p2p_set_robust_layout(code), "p2p_set_robust_layout")

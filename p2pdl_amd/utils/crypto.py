@@ -47,11 +47,15 @@ class KeyServer:
 
 
 def _ec():
+    """The EC half (out of scope, host): the `cryptography` package.  A
+    missing package raises ImportError -- the reference fails the same way,
+    at import (utils/crypto.py:1-3) -- it is never reported as a bad
+    signature."""
     try:
         from cryptography.hazmat.primitives import hashes
         from cryptography.hazmat.primitives.asymmetric import ec
         from cryptography.hazmat.primitives.asymmetric import utils as asym_utils
-    except ImportError as e:  # same failure the reference has without the package
+    except ImportError as e:
         raise ImportError("p2pdl_amd.utils.crypto: the EC step needs the 'cryptography' package") from e
     return hashes, ec, asym_utils
 
@@ -61,14 +65,18 @@ def _as_bytes(data) -> bytes:
 
 
 def digest_updates(messages: Sequence[bytes]) -> list[bytes]:
-    """SHA-256 of every message in one GPU launch (duplicates hashed once)."""
-    uniq, index = [], {}
+    """SHA-256 of every message in ONE GPU launch; a message that occurs
+    several times is hashed once (node/node.py:155,187-206 hash the same 3
+    updates 72 times per round)."""
+    uniq, index, slot = [], {}, []
     for m in messages:
-        if m not in index:
-            index[m] = len(uniq)
-            uniq.append(m)
+        key = m if isinstance(m, bytes) else bytes(m)
+        if key not in index:
+            index[key] = len(uniq)
+            uniq.append(key)
+        slot.append(index[key])
     d = ops.sha256_batch(uniq) if uniq else []
-    return [d[index[m]] for m in messages]
+    return [d[i] for i in slot]
 
 
 def generate_key_pair():
@@ -79,39 +87,70 @@ def generate_key_pair():
 
 
 def sign_data(private_key, data, digest: bytes | None = None):
-    """ECDSA(SHA-256(data)) like reference :50-59, digest computed on the GPU."""
+    """ECDSA(SHA-256(data)) like reference :50-59 -- the SHA-256 on the GPU,
+    the EC step on the 32-byte digest (Prehashed), which yields the same
+    signatures as ECDSA(SHA256()) over the data."""
     hashes, ec, asym_utils = _ec()
-    digest = digest if digest is not None else digest_updates([_as_bytes(data)])[0]
+    if digest is None:
+        if not isinstance(data, (bytes, bytearray, memoryview)):
+            raise TypeError(f"data must be bytes-like, got {type(data).__name__}")  # as cryptography's sign
+        digest = digest_updates([data])[0]
     return private_key.sign(digest, ec.ECDSA(asym_utils.Prehashed(hashes.SHA256())))
 
 
 def verify_signature(key_server, addr, port, data, signature, digest: bytes | None = None) -> bool:
-    """Reference :64-101 semantics: False on a missing key, None data, a
-    serialisation failure or a bad signature; never raises."""
+    """Reference :64-101: False on a missing key (:71-80), None data
+    (:83-85), a serialisation failure (:87-92) or a bad signature (:94-101).
+    ``digest`` (optional) is SHA-256(data) computed earlier, e.g. by
+    ``verify_signatures_batch``.  A missing GPU or `cryptography` raises."""
+    hashes, ec, asym_utils = _ec()
     public_key = key_server.get_key(addr, port)
     if not public_key:
         logging.error(f"Public key for {addr}:{port} not found.")
         return False
-    if data is None and digest is None:
-        logging.error(f"Cannot verify signature: data is None for {addr}:{port}")
-        return False
+    if digest is None:
+        if data is None:
+            logging.error(f"Cannot verify signature: data is None for {addr}:{port}")
+            return False
+        if not isinstance(data, bytes):
+            try:
+                data = pickle.dumps(data)
+            except Exception as e:
+                logging.error(f"Failed to serialize data for {addr}:{port}: {e}")
+                return False
+        digest = digest_updates([data])[0]
     try:
-        hashes, ec, asym_utils = _ec()
-        if digest is None:
-            digest = digest_updates([_as_bytes(data)])[0]
         public_key.verify(signature, digest, ec.ECDSA(asym_utils.Prehashed(hashes.SHA256())))
         return True
-    except Exception as e:  # reference returns False on any failure
+    except Exception as e:  # reference returns False on any verification failure
         logging.error(f"Signature verification failed for {addr}:{port}: {e}")
         return False
 
 
 def verify_signatures_batch(key_server, items: Iterable[tuple]) -> list[bool]:
-    """Verify many (addr, port, data, signature) at once: every distinct data
-    blob is hashed once in one GPU launch (node/node.py:187-206 verifies the
-    same bytes once per signature)."""
+    """verify_signature over many (addr, port, data, signature) items with
+    every distinct data blob hashed once, all in one GPU launch (the tester's
+    ready handler verifies the same bytes once per signature,
+    node/node.py:187-206).  Per-item results follow verify_signature."""
+    _ec()
     items = list(items)
-    blobs = [_as_bytes(d) for _, _, d, _ in items]
-    digests = digest_updates(blobs)
-    return [verify_signature(key_server, a, p, None, s, digest=g)
-            for (a, p, _, s), g in zip(items, digests)]
+    blobs, ok = [], []
+    for addr, port, data, _ in items:
+        if data is None:
+            blobs.append(None)
+            continue
+        try:
+            blobs.append(data if isinstance(data, bytes) else pickle.dumps(data))
+        except Exception as e:
+            logging.error(f"Failed to serialize data for {addr}:{port}: {e}")
+            blobs.append(None)
+    live = [b for b in blobs if b is not None]
+    digests = iter(digest_updates(live))
+    for (addr, port, data, sig), b in zip(items, blobs):
+        if b is None:
+            if data is None:
+                logging.error(f"Cannot verify signature: data is None for {addr}:{port}")
+            ok.append(False)
+            continue
+        ok.append(verify_signature(key_server, addr, port, None, sig, digest=next(digests)))
+    return ok

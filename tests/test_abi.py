@@ -33,21 +33,10 @@ def test_abi_version_and_argument_errors_without_gpu():
     assert L.p2p_abi_version() == N.ABI_VERSION
     assert L.p2p_strerror(0) == b"ok"
     assert b"invalid" in L.p2p_strerror(-1)
-    assert L.p2p_tile_elems(0, 3) == 4096 and L.p2p_tile_elems(1, 64) == 128
-    # robust: one lane per coordinate up to K = 128 (128-coordinate tiles);
-    # K in 129..256: 64-coordinate LDS-staged block tiles
-    assert L.p2p_tile_elems(1, 128) == 128 and L.p2p_tile_elems(1, 200) == 64 and L.p2p_tile_elems(2, 129) == 64
-    try:  # layout knob: LDS-staged kernels for K <= 128 too, and the legacy kernels
-        assert L.p2p_set_robust_layout(1) == 0 and L.p2p_tile_elems(1, 128) == 64 and L.p2p_tile_elems(1, 64) == 128
-        assert L.p2p_set_robust_layout(2) == 0 and L.p2p_tile_elems(1, 100) == 128
-        assert L.p2p_set_robust_layout(3) == 0 and L.p2p_tile_elems(1, 128) == 128 and L.p2p_tile_elems(1, 200) == 64
-        assert L.p2p_set_robust_layout(4) == 0 and L.p2p_tile_elems(1, 128) == 256 and L.p2p_tile_elems(1, 200) == 64
-        # radix16: 128-coordinate tiles for the median of exactly 256, else auto
-        assert L.p2p_set_robust_layout(5) == 0 and L.p2p_tile_elems(1, 256) == 128 and L.p2p_tile_elems(2, 256) == 64
-        assert L.p2p_tile_elems(1, 255) == 64 and L.p2p_tile_elems(1, 128) == 128
-        assert L.p2p_set_robust_layout(6) == -1
-    finally:
-        L.p2p_set_robust_layout(0)
+    # tile sizes are a pure function of (rule, k): no process-wide layout state
+    assert L.p2p_tile_elems(0, 3) == 1024 and L.p2p_tile_elems(0, 256) == 1024
+    assert L.p2p_tile_elems(1, 64) == 128 and L.p2p_tile_elems(1, 128) == 128
+    assert L.p2p_tile_elems(1, 129) == 64 and L.p2p_tile_elems(2, 200) == 64 and L.p2p_tile_elems(1, 256) == 64
     # argument validation happens before any HIP call
     assert L.p2p_fedavg_apply_f32(None, 3, 10, None, 0.1, None) == N.lib().p2p_aggregate_f32(
         None, 1, 1, 0, 0, 0.1, None, None, None) == -1

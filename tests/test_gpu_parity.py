@@ -160,6 +160,91 @@ def test_fedavg_large_k64_resnet_shape(cuda):
     assert_bits_equal(got[sl], w_ref, what="cfg2 tail")
 
 
+def resnet18_param_shapes():
+    """The 62 parameter tensors of torchvision's ResNet-18 (11,689,512
+    params, BASELINE cfg2), in state_dict order."""
+    shapes = [("conv1.weight", (64, 3, 7, 7)), ("bn1.weight", (64,)), ("bn1.bias", (64,))]
+    cin = 64
+    for li, cout in enumerate((64, 128, 256, 512), start=1):
+        for blk in range(2):
+            p = f"layer{li}.{blk}."
+            c0 = cin if blk == 0 else cout
+            shapes += [(p + "conv1.weight", (cout, c0, 3, 3)), (p + "bn1.weight", (cout,)), (p + "bn1.bias", (cout,)),
+                       (p + "conv2.weight", (cout, cout, 3, 3)), (p + "bn2.weight", (cout,)), (p + "bn2.bias", (cout,))]
+            if blk == 0 and cin != cout:
+                shapes += [(p + "downsample.0.weight", (cout, cin, 1, 1)), (p + "downsample.1.weight", (cout,)),
+                           (p + "downsample.1.bias", (cout,))]
+        cin = cout
+    shapes += [("fc.weight", (1000, 512)), ("fc.bias", (1000,))]
+    assert len(shapes) == 62 and sum(int(np.prod(s)) for _, s in shapes) == 11_689_512
+    return shapes
+
+
+@pytest.mark.parametrize("rule", ["fedavg", "median", "trimmed"])
+def test_dropin_cfg2_resnet18_full_size(cuda, rule, monkeypatch):
+    """VERDICT r01 missing: cfg2 at full size THROUGH the drop-in boundary --
+    aggregate_models on a ResNet-18 parameter state_dict (62 tensors,
+    11,689,512 fp32) with 64 updates (one segment-table launch), every output
+    coordinate compared with the oracle (reference aggregation.py:7-46)."""
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
+    shapes = resnet18_param_shapes()
+    k, n, seed = 64, 11_689_512, 0x5EED0001
+    slab = torch.empty((k, n), dtype=torch.float32, device=cuda)
+    for p in range(k):
+        ops.fill_synthetic_(slab[p], seed, p, 1e-2)
+    w = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.fill_synthetic_(w, seed, 0xFFFFF, 5e-2)
+    offs = np.cumsum([0] + [int(np.prod(s)) for _, s in shapes])
+
+    def as_dict(vec):
+        return {nm.replace(".", "__"): vec[offs[i]:offs[i + 1]].view(s) for i, (nm, s) in enumerate(shapes)}
+
+    model = Holder(shapes).to(cuda)
+    with torch.no_grad():
+        model.load_state_dict(as_dict(w))
+    node = fake_node(model, [as_dict(slab[p]) for p in range(k)])
+    agg.aggregate_models(node, rule=rule)
+    got = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+    del slab
+    torch.cuda.empty_cache()
+    peers = [oracle.synth(n, seed, p, 1e-2) for p in range(k)]
+    w0 = oracle.synth(n, seed, 0xFFFFF, 5e-2)
+    if rule == "fedavg":
+        want, _ = oracle.fedavg(peers, w0)
+    else:
+        r = ops.rule_id(rule)
+        want, _ = oracle.robust(peers, r, ops.trim_count(k) if r == 2 else 0, w=w0)
+    assert_bits_equal(got, want, what=f"cfg2 drop-in {rule}")
+    assert node.received_models == []
+
+
+def test_dropin_widens_half_updates_and_rejects_float64(cuda, monkeypatch):
+    """fp16 / bf16 updates widen to fp32 exactly (what the reference's fp32
+    `acc += u` computes in); fp64 updates are refused -- the reference adds
+    those in fp64 and rounds once."""
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
+    shapes = [("fc.weight", (8, 16)), ("fc.bias", (8,))]
+    n = 136
+    w = oracle.synth(n, 31, 0xFFFFF, 5e-2)
+    peers = [oracle.synth(n, 31, p, 1.0) for p in range(3)]
+    halves = [p.astype(np.float16) for p in peers]
+    model = Holder(shapes).to(cuda)
+    with torch.no_grad():
+        model.load_state_dict(split(w, shapes, cuda))
+    upd = [{k: v.half() for k, v in split(h.astype(np.float32), shapes, cuda).items()} for h in halves]
+    agg.aggregate_models(fake_node(model, upd))
+    got = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+    want, _ = oracle.fedavg([h.astype(np.float32) for h in halves], w)
+    assert_bits_equal(got, want, what="fp16 updates")
+    bad = [{k: v.double() for k, v in split(p, shapes, cuda).items()} for p in peers]
+    with pytest.raises(TypeError):
+        agg.aggregate_models(fake_node(model, bad))
+
+
 def test_fedavg_devk(cuda):
     n, k = 9999, 6
     peers = [to_dev(oracle.synth(n, 5, p, 1e-2), cuda) for p in range(k)]
@@ -178,15 +263,16 @@ def special_peers(k, n, seed):
     sp = np.array([0.0, -0.0, 1e-45, -1e-45, np.inf, -np.inf, np.nan, -np.nan, 1.0, -1.0,
                    3.4e38, -3.4e38, 0.5, 0.25], dtype=np.float32)
     peers = []
-    for p in range(k):
-        x = oracle.synth(n, seed, p, 1e-2)
-        x[: n // 4] = np.round(x[: n // 4] * 2 ** 8) / 2 ** 8 * 0  # ties (many zeros of both signs)
-        x[: n // 8] = np.where(rng.random(n // 8) < 0.5, np.float32(-0.0), np.float32(0.0))
-        m = rng.random(n) < 0.05
-        x[m] = rng.choice(sp, size=int(m.sum()))
-        q = slice(n // 4, n // 2)
-        x[q] = np.round(x[q] * 2 ** 6) / 2 ** 6  # quantised: many equal keys
-        peers.append(x.astype(np.float32))
+    with np.errstate(all="raise"):  # the case must not lose its finite extremes to overflow
+        for p in range(k):
+            x = oracle.synth(n, seed, p, 1e-2)
+            x[: n // 4] = 0.0  # ties (many zeros of both signs)
+            x[: n // 8] = np.where(rng.random(n // 8) < 0.5, np.float32(-0.0), np.float32(0.0))
+            q = slice(n // 4, n // 2)
+            x[q] = np.round(x[q] * 2 ** 6) / 2 ** 6  # quantised: many equal keys
+            m = rng.random(n) < 0.05  # specials last, so +-3.4e38 stay finite in every stripe
+            x[m] = rng.choice(sp, size=int(m.sum()))
+            peers.append(x.astype(np.float32))
     return peers
 
 
@@ -206,46 +292,34 @@ def test_robust_vs_oracle(cuda, rule, k):
     assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k}")
 
 
-@pytest.fixture(params=["auto", "lds", "lds2", "lds1", "group", "radix16"])
-def robust_layout(request):
-    ops.set_robust_layout(request.param)
-    yield request.param
-    ops.set_robust_layout("auto")
-
-
 @pytest.mark.parametrize("rule", ["median", "trimmed"])
 @pytest.mark.parametrize("k", [65, 96, 128, 129, 160, 256])
-def test_robust_layouts_many_tiles(cuda, robust_layout, rule, k):
-    """Every K in 65..256 layout over many tiles per wave (persistent loop with
-    the next tile's LDS-DMA in flight) and a ragged tail tile."""
+def test_robust_many_tiles(cuda, rule, k):
+    """K in 65..256 over many tiles per block (persistent loop with the next
+    tile's LDS-DMA in flight for K > 128) and a ragged tail tile."""
     peers, w, b, w_ref, out_ref = _many_tiles_case(rule, k)
     n = w.size
     wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
     ops.aggregate([to_dev(p, cuda) for p in peers], rule, w=wt, out=out, trim_b=b)
-    assert_bits_equal(host(out), out_ref, nan_equal=(rule != "median"), what=f"{robust_layout} {rule} K={k}")
-    assert_bits_equal(host(wt), w_ref, what=f"{robust_layout} {rule} apply K={k}")
-
-
-_MANY = {}
+    assert_bits_equal(host(out), out_ref, nan_equal=(rule != "median"), what=f"{rule} K={k}")
+    assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k}")
 
 
 def _many_tiles_case(rule, k):
-    if (rule, k) not in _MANY:  # the oracle runs once per case, not per layout
-        n = 200_003
-        peers = [oracle.synth(n, 5 * k, p, 1e-2) for p in range(k)]
-        for p in range(0, k, 7):  # ties and special values in a stripe
-            peers[p][1000:1100] = peers[0][1000:1100]
-            peers[p][2000:2003] = np.array([np.inf, -0.0, np.nan], dtype=np.float32)
-        w = oracle.synth(n, 5, 0xFFFFF, 5e-2)
-        b = ops.trim_count(k) if rule == "trimmed" else 0
-        w_ref, out_ref = oracle.robust(peers, ops.rule_id(rule), b, w=w)
-        _MANY[(rule, k)] = (peers, w, b, w_ref, out_ref)
-    return _MANY[(rule, k)]
+    n = 200_003
+    peers = [oracle.synth(n, 5 * k, p, 1e-2) for p in range(k)]
+    for p in range(0, k, 7):  # ties and special values in a stripe
+        peers[p][1000:1100] = peers[0][1000:1100]
+        peers[p][2000:2003] = np.array([np.inf, -0.0, np.nan], dtype=np.float32)
+    w = oracle.synth(n, 5, 0xFFFFF, 5e-2)
+    b = ops.trim_count(k) if rule == "trimmed" else 0
+    w_ref, out_ref = oracle.robust(peers, ops.rule_id(rule), b, w=w)
+    return peers, w, b, w_ref, out_ref
 
 
 @pytest.mark.parametrize("rule", ["median", "trimmed"])
 @pytest.mark.parametrize("k", [100, 256])
-def test_robust_unaligned_views(cuda, robust_layout, rule, k):
+def test_robust_unaligned_views(cuda, rule, k):
     """Peer views at odd float offsets cannot be LDS-DMA'd (16-B pieces): the
     register-staged fill must give the same bits."""
     n = 50_001
@@ -263,7 +337,7 @@ def test_robust_unaligned_views(cuda, robust_layout, rule, k):
 
 @pytest.mark.parametrize("rule", ["median", "trimmed"])
 @pytest.mark.parametrize("k", [72, 256])
-def test_robust_segments_layouts(cuda, robust_layout, rule, k):
+def test_robust_segments(cuda, rule, k):
     """One launch over a state_dict of ragged tensors (segment table)."""
     sizes = [1, 15, 16, 17, 4099, 33_333, 100_000]
     n = sum(sizes)
@@ -276,7 +350,7 @@ def test_robust_segments_layouts(cuda, robust_layout, rule, k):
     pl = [[to_dev(p[offs[i]:offs[i + 1]], cuda) for i in range(len(sizes))] for p in peers]
     ops.aggregate_segments_(ws, pl, rule)
     got = np.concatenate([host(t) for t in ws])
-    assert_bits_equal(got, w_ref, what=f"segments {robust_layout} {rule} K={k}")
+    assert_bits_equal(got, w_ref, what=f"segments {rule} K={k}")
 
 
 @pytest.mark.parametrize("k,b", [(5, 0), (5, 2), (10, 3), (128, 0), (128, 63), (200, 10), (256, 51), (256, 100)])

@@ -4,6 +4,8 @@ CPU tests pin the restricted parser to pickle.loads on torch-produced
 pickles of the reference's message shapes (node/node.py:285 pickles a
 state_dict of the models/model.py MLP); GPU tests land updates in the device
 slab and aggregate them through the drop-in."""
+import collections
+import io
 import os
 import pickle
 import socket
@@ -16,7 +18,7 @@ import torch
 
 import oracle
 from helpers import assert_bits_equal
-from p2pdl_amd.node.inbox import DeviceInbox, UpdateParser, ZeroCopyParser, recv_message
+from p2pdl_amd.node.inbox import DeviceInbox, ZeroCopyParser, recv_message
 
 MLP_SHAPES = [("fc1.weight", (512, 784)), ("fc1.bias", (512,)), ("fc2.weight", (256, 512)),
               ("fc2.bias", (256,)), ("fc3.weight", (10, 256)), ("fc3.bias", (10,))]  # models/model.py:6-8
@@ -38,10 +40,10 @@ def same(raw, ref):
         assert a.dtype == r.dtype and np.array_equal(a.view(np.uint8), r.view(np.uint8)), k
 
 
-PARSERS = [UpdateParser.parse, lambda d: ZeroCopyParser(d).parse()]
+PARSERS = [lambda d: ZeroCopyParser(d).parse()]
 
 
-@pytest.mark.parametrize("parse", PARSERS, ids=["c-unpickler", "zero-copy"])
+@pytest.mark.parametrize("parse", PARSERS, ids=["zero-copy"])
 def test_parser_matches_pickle_loads_mlp_update(parse):
     upd = mlp_update(1)
     data = pickle.dumps(upd)  # reference node/node.py:285
@@ -49,7 +51,7 @@ def test_parser_matches_pickle_loads_mlp_update(parse):
 
 
 @pytest.mark.parametrize("proto", [3, 4, 5])
-@pytest.mark.parametrize("parse", PARSERS, ids=["c-unpickler", "zero-copy"])
+@pytest.mark.parametrize("parse", PARSERS, ids=["zero-copy"])
 def test_parser_batchnorm_scalars_views_and_ordereddict(parse, proto):
     net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.BatchNorm1d(5))
     sd = net.state_dict()  # OrderedDict incl. an int64 0-d buffer
@@ -91,8 +93,143 @@ def test_zero_copy_parser_rejects_protocol_2_and_truncation():
     with pytest.raises(pickle.UnpicklingError):
         ZeroCopyParser(pickle.dumps({"a": torch.ones(2)}, protocol=2)).parse()
     data = pickle.dumps({"a": torch.ones(2)})
-    with pytest.raises((pickle.UnpicklingError, IndexError, ValueError)):
-        ZeroCopyParser(data[:-20]).parse()
+    for cut in range(1, len(data)):  # every truncation: UnpicklingError and nothing else
+        for parse in PARSERS:
+            with pytest.raises(pickle.UnpicklingError):
+                parse(data[:cut])
+
+
+def test_parsers_raise_only_unpickling_error_on_corrupted_bytes():
+    """A listener catching pickle.UnpicklingError must survive any peer bytes
+    (KeyError / IndexError / struct.error used to escape)."""
+    rng = np.random.default_rng(0)
+    data = pickle.dumps(torch.nn.Sequential(torch.nn.Linear(3, 2), torch.nn.BatchNorm1d(2)).state_dict())
+    for _ in range(3000):
+        m = bytearray(data)
+        for i in rng.integers(0, len(m), rng.integers(1, 4)):
+            m[i] = int(rng.integers(0, 256))
+        for parse in PARSERS:
+            try:
+                parse(bytes(m))
+            except pickle.UnpicklingError:
+                pass
+
+
+# ---- forged updates: the storage blob and the tensor view come from the peer
+def _good_blob(n=2):
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        fn, (blob,) = torch.ones(n).storage().__reduce__()  # what torch pickles per tensor
+    assert fn is torch.storage._load_from_bytes
+    return blob
+
+
+class _Storage:
+    def __init__(self, blob):
+        self.blob = blob
+
+    def __reduce__(self):
+        return (torch.storage._load_from_bytes, (self.blob,))
+
+
+class _Tensor:
+    def __init__(self, blob, offset=0, size=(2,), stride=(1,)):
+        self.args = (_Storage(blob), offset, size, stride, False, collections.OrderedDict())
+
+    def __reduce__(self):
+        return (torch._utils._rebuild_tensor_v2, self.args)
+
+
+def _forged(blob, **view):
+    return pickle.dumps({"a": _Tensor(blob, **view)})
+
+
+def test_forged_update_with_honest_view_parses():
+    data = _forged(_good_blob(4), offset=1, size=(3,), stride=(1,))
+    for parse in PARSERS:
+        raw = parse(data)
+        assert raw["a"].array().tolist() == [1.0, 1.0, 1.0]
+
+
+@pytest.mark.parametrize("which", [0, 1, 2])
+def test_storage_header_pickles_cannot_run_code(which, tmp_path):
+    """the magic / protocol-version / sys_info pickles of
+    the storage blob went through a plain pickle.Unpickler.  A GLOBAL/REDUCE
+    nested in any of them must be refused, and must not run."""
+    blob = _good_blob()
+    f = io.BytesIO(blob)
+    starts = [0]
+    for _ in range(3):  # the three header pickles precede the storage record
+        pickle.Unpickler(f).load()  # our own, honest blob
+        starts.append(f.tell())
+    marker = tmp_path / "pwned"
+    evil = pickle.dumps(_Touch(str(marker)))
+    forged = blob[:starts[which]] + evil + blob[starts[which + 1]:]
+    for parse in PARSERS:
+        with pytest.raises(pickle.UnpicklingError):
+            parse(_forged(forged))
+    assert not marker.exists()
+
+
+class _Touch:
+    def __init__(self, path):
+        self.path = path
+
+    def __reduce__(self):
+        return (open, (self.path, "w"))
+
+
+@pytest.mark.parametrize("view", [
+    dict(size=(1000,)),                       # more elements than the storage holds
+    dict(offset=5, size=(1,)),                # offset past the end
+    dict(offset=1, size=(2,)),                # last element one past the end
+    dict(size=(2, 2), stride=(1, 1)),         # strided view reaching element 2
+    dict(size=(2,), stride=(-1,)),            # negative stride
+    dict(offset=-1, size=(1,)),               # negative offset
+    dict(size=(2,), stride=(1, 1)),           # rank mismatch
+    dict(size=(2.0,)),                        # non-integer size
+])
+def test_out_of_bounds_tensor_views_are_refused(view):
+    """a peer claiming a view larger than its storage made
+    as_strided read host memory past the message."""
+    data = _forged(_good_blob(2), **view)
+    for parse in PARSERS:
+        with pytest.raises(pickle.UnpicklingError):
+            parse(data)
+
+
+def test_build_cannot_shadow_dict_methods():
+    """A pickle's BUILD on the OrderedDict may set only torch's `_metadata`."""
+    class Shadow(collections.OrderedDict):
+        def __reduce__(self):
+            return (collections.OrderedDict, (), {"values": None}, None, iter(self.items()))
+
+    d = Shadow()
+    d["a"] = torch.ones(2)
+    data = pickle.dumps(d)
+    with pytest.raises(pickle.UnpicklingError):
+        ZeroCopyParser(data).parse()
+    raw = ZeroCopyParser(pickle.dumps(torch.nn.Linear(2, 2).state_dict())).parse()
+    assert type(raw) is collections.OrderedDict and not raw.__dict__  # a fresh dict
+
+
+def test_huge_memo_index_is_cheap():
+    """A LONG_BINPUT with a ~1.5e9 index made the C unpickler allocate a
+    12 GB memo array (found by the corruption fuzz above); the machine's
+    memo is a dict."""
+    import time
+
+    data = bytearray(pickle.dumps({"b": torch.ones(2)}))
+    i = data.index(b"\x94", data.index(b"_rebuild_tensor_v2"))  # a MEMOIZE after the global
+    data[i:i + 1] = b"r\xff\xff\xff\x5f"  # LONG_BINPUT 0x5fffffff
+    t0 = time.perf_counter()
+    try:
+        ZeroCopyParser(bytes(data)).parse()
+    except pickle.UnpicklingError:
+        pass
+    assert time.perf_counter() - t0 < 1.0
 
 
 def test_recv_message_framing_and_early_close():
@@ -198,3 +335,34 @@ def test_broadcast_from_gpu_model_one_transfer(cuda):
     for k, v in ref.items():
         assert torch.equal(msg["model"][k], v.cpu()), k
         assert msg["model"][k].untyped_storage().nbytes() == v.numel() * v.element_size(), k
+
+
+@pytest.mark.gpu
+def test_device_inbox_concurrent_landing(cuda):
+    """land() is called from one listener thread per connection
+    (reference node/node.py:89); concurrent calls must take distinct rows and
+    never mix two updates in a staging row."""
+    k = 8
+    template = {name: torch.zeros(s, device=cuda) for name, s in MLP_SHAPES}
+    inbox = DeviceInbox(template, k_max=k, device=cuda)
+    ser = [pickle.dumps(mlp_update(40 + j)) for j in range(k)]
+    got = [None] * k
+    barrier = threading.Barrier(k)
+
+    def worker(j):
+        barrier.wait()
+        got[j] = inbox.land(ser[j])
+
+    ths = [threading.Thread(target=worker, args=(j,)) for j in range(k)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(60)
+    torch.cuda.synchronize()
+    assert inbox.count == k
+    rows = {got[j]["fc1.weight"].data_ptr() for j in range(k)}
+    assert len(rows) == k  # every update in its own slab row
+    for j in range(k):
+        ref = pickle.loads(ser[j])
+        for key in ref:
+            assert_bits_equal(got[j][key].cpu().numpy(), ref[key].numpy(), what=f"update {j} {key}")

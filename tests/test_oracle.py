@@ -106,3 +106,38 @@ def test_synth_at_matches_synth():
     idx = np.array([0, 1, 17, 4095, 99_999])
     full = oracle.synth(100_000, 0x5EED0001, 3, 1e-2)
     assert np.array_equal(oracle.synth_at(idx, 0x5EED0001, 3, 1e-2), full[idx])
+
+
+@pytest.mark.parametrize("k", [5, 10, 128, 256])
+def test_trimmed_mean_oracle_pinned_to_scipy_bit_exact(k):
+    """External pin of the build-defined trimmed mean:
+    scipy.stats.trim_mean(x, 0.2, axis=0) cuts int(0.2 K) per end, as
+    trim_count does.  With integer-valued fp32 inputs every partial sum is
+    exact (|sum| < 2**24), so summation order cannot matter and the fp32
+    quotients must agree bit for bit."""
+    from scipy import stats
+
+    n = 20_000
+    rng = np.random.default_rng(k)
+    x = rng.integers(-1000, 1001, size=(k, n)).astype(np.float32)
+    x[:, :500] = rng.integers(-3, 4, size=(k, 500))  # heavy ties
+    b = oracle.trim_count(k)
+    assert b == int(0.2 * k)
+    _, got = oracle.robust(list(x), oracle.RULE_TRIMMED, b)
+    want = stats.trim_mean(x, 0.2, axis=0)
+    assert want.dtype == np.float32
+    assert_bits_equal(got, want, what=f"trim_mean K={k}")
+    assert_bits_equal(oracle.robust_np(list(x), oracle.RULE_TRIMMED, b), want, what=f"numpy K={k}")
+
+
+@pytest.mark.parametrize("k", [5, 10, 128, 255, 256])
+def test_median_oracle_pinned_to_torch_median_integer_ties(k):
+    """torch.median (lower median for even K) on integer-valued data with
+    many ties, both signs (NaN-free: torch propagates NaN, the key order ranks
+    it)."""
+    n = 20_000
+    rng = np.random.default_rng(100 + k)
+    x = rng.integers(-50, 51, size=(k, n)).astype(np.float32)
+    _, got = oracle.robust(list(x), oracle.RULE_MEDIAN)
+    want = torch.from_numpy(x).median(dim=0).values.numpy()
+    assert_bits_equal(got, want, nan_equal=False, what=f"median K={k}")

@@ -91,3 +91,66 @@ def test_gloo_world2_byte_identical_to_single(rule, n, k, chunk):
         rid = 1 if rule == "median" else 2
         want, _ = oracle.robust(peers, rid, oracle.trim_count(k) if rid == 2 else 0, w=w)
     assert got[0] == got[1] == want.tobytes()
+
+
+# ---------------------------------------------------------------- GPU leg
+def _gpu_worker(rank, world, port, n, k, rule, chunk, overlap, q):
+    """One rank: the HIP reduce (the default of sharded_aggregate_) on cuda:0,
+    gloo for the all-gather (both ranks share the one GPU of the test box;
+    the driver's multi-GPU bench uses RCCL)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        peers = [torch.from_numpy(oracle.synth(n, 23, p, 1e-2)).to(dev) for p in range(k)]
+        w = torch.from_numpy(oracle.synth(n, 23, 0xFFFFF, 5e-2)).to(dev)
+        plan = sharded_aggregate_(w, peers, rule=rule, chunk=chunk, overlap=overlap)
+        torch.cuda.synchronize()
+        q.put((rank, w.cpu().numpy().tobytes(), plan.full_rounds, plan.tail))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # report, do not hang the parent
+        q.put((rank, repr(e), -1, -1))
+        raise
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule,n,k,chunk,overlap", [
+    ("fedavg", 100_003, 9, 8192, True),     # 6 full rounds + ragged tail, gather on a comm stream
+    ("fedavg", 65_536, 256, 16_384, False),  # no tail, K = 256
+    ("median", 50_001, 130, 4096, True),    # LDS-staged robust kernel (K > 128)
+    ("trimmed", 50_001, 64, 6000, True),    # one-lane robust kernel, unaligned chunk starts
+    ("trimmed", 30_011, 256, 4096, True),
+])
+def test_gpu_world2_hip_reduce_byte_identical_to_oracle(cuda, rule, n, k, chunk, overlap):
+    """VERDICT r01 missing #2: sharded_aggregate_ with the DEFAULT (HIP)
+    per-shard reduce -- each rank reduces its round-robin chunks on the GPU,
+    the all-gather reassembles -- byte-compared with the CPU oracle on both
+    ranks (reference aggregation.py:25-38 is coordinate-wise)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, n, k, rule, chunk, overlap, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, b, rounds, tail = q.get(timeout=180)
+        assert isinstance(b, bytes), f"rank {r} failed: {b}"
+        got[r] = b
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert rounds >= 1 and (tail > 0) == (n % (2 * chunk) != 0)
+    peers = [oracle.synth(n, 23, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, 23, 0xFFFFF, 5e-2)
+    if rule == "fedavg":
+        want, _ = oracle.fedavg(peers, w)
+    else:
+        rid = 1 if rule == "median" else 2
+        want, _ = oracle.robust(peers, rid, oracle.trim_count(k) if rid == 2 else 0, w=w)
+    assert got[0] == got[1], "ranks disagree after the all-gather"
+    g = np.frombuffer(got[0], dtype=np.uint32)
+    bad = np.nonzero(g != want.view(np.uint32))[0]
+    assert bad.size == 0, f"{bad.size} coordinates differ, first {bad[:5]}"
