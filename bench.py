@@ -404,11 +404,20 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
     with torch.no_grad():
         for i, p in enumerate(model.parameters()):
             p.view(-1).copy_(flat_w[offs[i]:offs[i + 1]])
-    slab = torch.empty((K, n), dtype=torch.float32, device=dev)
+    # the updates live where DeviceInbox lands received updates: rows of one
+    # [K, N] slab (every tensor size here is a multiple of 4, so the row
+    # layout is the plain concatenation), generated on device
+    from p2pdl_amd.node.inbox import DeviceInbox
+
+    inbox = DeviceInbox(model.state_dict(), k_max=K, device=dev)
+    assert inbox.row == n
+    slab = inbox.slab
     for p in range(K):
         ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE)
+    landed = [inbox.view(j) for j in range(K)]
     keys = [nm.replace(".", "__") for nm, _ in shapes]
-    updates = [{k: slab[j, offs[i]:offs[i + 1]].view(shapes[i][1]) for i, k in enumerate(keys)} for j in range(K)]
+    plain = [{k: slab[j, offs[i]:offs[i + 1]].view(shapes[i][1]) for i, k in enumerate(keys)} for j in range(K)]
+    updates = landed
     node = types.SimpleNamespace(model=model, trainers_list=[0] * K, addr="127.0.0.1", port=1, neighbors=[],
                                  received_models=[])
     saved = agg.broadcast_global_model_update
@@ -448,9 +457,21 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
             call(record=True)
         torch.cuda.synchronize()
         step_s = (time.perf_counter() - t0) / steps
+        ev_fast = list(ev)
+        # the general path (plain dicts of tensors, e.g. from pickle.loads):
+        # per-tensor checks on the host for all L x K update tensors
+        updates = plain
+        call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call()
+        torch.cuda.synchronize()
+        general_s = (time.perf_counter() - t0) / steps
+        ev.clear()
     finally:
         agg.broadcast_global_model_update = saved
-    call_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    call_ms = sum(a.elapsed_time(b) for a, b in ev_fast) / len(ev_fast)
     # the same bytes through the flat C-ABI kernel (one buffer per peer), for comparison
     table = ops.pointer_table(list(slab), dev)
     fe = []
@@ -463,7 +484,7 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
             fe.append((e0, e1))
     torch.cuda.synchronize()
     flat_ms = sum(a.elapsed_time(b) for a, b in fe) / len(fe)
-    del slab, flat_w, table, updates, model
+    del slab, flat_w, table, updates, model, inbox, landed, plain
     torch.cuda.empty_cache()
     cpu = None
     if not args.no_cpu_baseline and cpu_s > 0:
@@ -475,10 +496,12 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
                                               f"CPU, {res['reps']} reps in {res['seconds']}s")
     return {
         "workload": name.replace("-", "_"), "value": round(K * n * 4 / step_s / 1e9, 2), "unit": "GB/s",
-        "ms_per_step": round(step_s * 1e3, 4), "us_per_call": round(step_s * 1e6, 1), "steps": steps,
+        "ms_per_step": round(step_s * 1e3, 4), "us_per_call": round(step_s * 1e6, 1),
+        "us_per_call_general_path": round(general_s * 1e6, 1), "steps": steps,
         "scaling": "weak", "dtype": "fp32",
         "config": {"workload": f"{name}: drop-in aggregate_models, {len(sizes)}-tensor state_dict "
-                               f"({n:,} params) x {K} updates, one segment-table launch per call",
+                               f"({n:,} params) x {K} updates landed in a DeviceInbox slab, one "
+                               f"segment-table launch per call",
                    "peers": K, "coords_per_gpu": n, "tensors": len(sizes), "parallelism": "single GPU"},
         "roofline": roofline(4 * n * (K + 2), call_ms, traffic_for(name, n, K),
                              timing="HIP events around aggregate_models (table H2D + segment kernel)",

@@ -55,6 +55,11 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
 
     state = self.model.state_dict()
     keys = list(state.keys())
+    if _slab_fast_path(state, keys, received, rule or AGGREGATION_RULE, lr, trim_frac):
+        logging.info(f"[{self.addr}:{self.port}] Model aggregation completed, applied local updates.")
+        self.received_models.clear()
+        broadcast_global_model_update(self)
+        return
     updates = []
     for received_model in received:  # KeyError on a missing key, like :28
         local_update = received_model["model"]
@@ -69,24 +74,17 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
             raise NotImplementedError(f"p2pdl_amd aggregates float32 state_dicts; {key} is {t.dtype}")
 
     ws = [state[key] for key in keys]
+    numels = [w.numel() for w in ws]
+    dev = ws[0].device if ws else None
+    di = dev.index if dev is not None else None
+    f32 = torch.float32
     peer_lists = []
-    for j, upd in enumerate(updates):
-        row = []
-        for key, w, u in zip(keys, ws, upd):
-            if u.device != w.device:
-                raise RuntimeError(f"Expected all tensors to be on the same device, but found at least "
-                                   f"two devices, {w.device} and {u.device}! (update {j}, key {key})")
-            if u.numel() != w.numel():
-                raise RuntimeError(f"update {j} key {key}: {tuple(u.shape)} does not match "
-                                   f"{tuple(w.shape)}")
-            if u.dtype != torch.float32:
-                if u.dtype == torch.float64 or u.is_complex():
-                    # the reference's in-place `acc += u` (:28) adds in float64 and rounds
-                    # once; casting u to fp32 first would round twice (1-ulp differences)
-                    raise TypeError(f"update {j} key {key} is {u.dtype}; p2pdl_amd aggregates float32 "
-                                    f"updates (fp16 / bf16 / integer updates are widened exactly)")
-                u = u.to(torch.float32)  # exact widening: what the reference's add computes in
-            row.append(u.contiguous())
+    for j, row in enumerate(updates):
+        # one pass of cheap getters; the per-tensor diagnosis and the exact
+        # widening of fp16 / bf16 / integer updates only when needed
+        if not all(u.dtype is f32 and u.get_device() == di and u.numel() == n and u.is_contiguous()
+                   for u, n in zip(row, numels)):
+            row = [_checked_update(j, key, w, u) for key, w, u in zip(keys, ws, row)]
         peer_lists.append(row)
 
     # state_dict() tensors are views of the parameters: updating them in place
@@ -104,6 +102,57 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
 
     # Broadcast the newly aggregated global model (:46)
     broadcast_global_model_update(self)
+
+
+def _checked_update(j, key, w, u):
+    if u.device != w.device:
+        raise RuntimeError(f"Expected all tensors to be on the same device, but found at least "
+                           f"two devices, {w.device} and {u.device}! (update {j}, key {key})")
+    if u.numel() != w.numel():
+        raise RuntimeError(f"update {j} key {key}: {tuple(u.shape)} does not match {tuple(w.shape)}")
+    if u.dtype != torch.float32:
+        if u.dtype == torch.float64 or u.is_complex():
+            # the reference's in-place `acc += u` (:28) adds in float64 and rounds
+            # once; casting u to fp32 first would round twice (1-ulp differences)
+            raise TypeError(f"update {j} key {key} is {u.dtype}; p2pdl_amd aggregates float32 "
+                            f"updates (fp16 / bf16 / integer updates are widened exactly)")
+        u = u.to(torch.float32)  # exact widening: what the reference's add computes in
+    return u.contiguous()
+
+
+def _slab_fast_path(state, keys, received, rule, lr, trim_frac) -> bool:
+    """Updates landed by node.inbox.DeviceInbox (frozen LandedUpdate dicts
+    whose fp32 tensors are rows of one device slab): the kernel table comes
+    from (slab, rows, key offsets) in one broadcast -- no per-tensor Python
+    work for the L x K update tensors.  Returns False (general path, with the
+    reference's error behaviour) unless every condition holds: all updates
+    from one inbox, every model key a slab entry of every update, model
+    tensors fp32 contiguous on the slab's device with the slab layout's
+    element counts."""
+    from ..node.inbox import LandedUpdate
+
+    if not received:
+        return False
+    first = received[0].get("model") if isinstance(received[0], dict) else None
+    if not isinstance(first, LandedUpdate):
+        return False
+    inbox = first.inbox
+    for rm in received:
+        u = rm.get("model") if isinstance(rm, dict) else None
+        if not isinstance(u, LandedUpdate) or u.inbox is not inbox or not u.slab_keys.issuperset(keys):
+            return False
+    layout, dev = inbox.layout, inbox.slab.device
+    ws, offsets = [], []
+    for key in keys:
+        t = state[key]
+        off, _, n = layout[key]
+        if t.dtype != torch.float32 or t.device != dev or not t.is_contiguous() or t.numel() != n:
+            return False
+        ws.append(t)
+        offsets.append(off)
+    ops.aggregate_slab_rows_(ws, inbox.slab, [rm["model"].row for rm in received], offsets, rule,
+                             lr=lr, trim_frac=trim_frac)
+    return True
 
 
 _PINNED = {}  # (device, numel) -> pinned host staging buffer, reused across rounds

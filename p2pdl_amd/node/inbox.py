@@ -449,6 +449,58 @@ def recv_message(conn) -> bytearray | None:
     return data
 
 
+class LandedUpdate(OrderedDict):
+    """What DeviceInbox.land returns: {key: tensor} in the update's key order,
+    the fp32 entries views of ONE slab row.  It is frozen (every mutator
+    raises TypeError), so the aggregator can trust that the entries listed in
+    ``slab_keys`` are still slab[row, offset : offset + numel] and build its
+    kernel table from (slab, row, layout) without inspecting each tensor
+    (ops.aggregate_slab_rows_)."""
+
+    def __init__(self, items, inbox: "DeviceInbox", row: int, slab_keys: frozenset):
+        super().__init__(items)
+        self.inbox, self.row, self.slab_keys = inbox, row, slab_keys
+        self._frozen = True
+
+    def _refuse(self, *a, **k):
+        if getattr(self, "_frozen", False):
+            raise TypeError("a landed update is read-only (its tensors are slab views)")
+
+    def __setitem__(self, key, value):
+        self._refuse()
+        super().__setitem__(key, value)
+
+    def __delitem__(self, key):
+        self._refuse()
+        super().__delitem__(key)
+
+    def clear(self):
+        self._refuse()
+
+    def pop(self, *a):
+        self._refuse()
+
+    def popitem(self, *a, **k):
+        self._refuse()
+
+    def setdefault(self, *a):
+        self._refuse()
+
+    def update(self, *a, **k):
+        self._refuse()
+
+    def move_to_end(self, *a, **k):
+        self._refuse()
+
+    def __ior__(self, other):
+        self._refuse()
+
+    def __reduce__(self):
+        # a plain OrderedDict of copies: pickling a slab view would carry the
+        # whole slab (torch pickles a view's entire storage)
+        return (OrderedDict, ([(k, v.clone()) for k, v in self.items()],))
+
+
 class DeviceInbox:
     """[K_max, N] fp32 slab on the GPU for the updates of one round.
 
@@ -521,12 +573,23 @@ class DeviceInbox:
             ev = torch.cuda.Event()
             ev.record()
             self._events[s] = ev
+        slab_keys = []
         for key in raw:
             if key in out:
                 continue
             off, shape, n = self.layout[key]
             out[key] = row[off:off + n].view(shape)
-        return OrderedDict((key, out[key]) for key in raw)
+            slab_keys.append(key)
+        return LandedUpdate(((key, out[key]) for key in raw), self, k, frozenset(slab_keys))
+
+    def view(self, k: int) -> LandedUpdate:
+        """Row k as a landed update holding every fp32 key of the template
+        (for rows filled on the device, e.g. by synthetic generators)."""
+        if not 0 <= k < self.k_max:
+            raise IndexError(f"slab row {k} out of range (k_max={self.k_max})")
+        row = self.slab[k]
+        items = [(key, row[off:off + n].view(shape)) for key, (off, shape, n) in self.layout.items()]
+        return LandedUpdate(items, self, k, frozenset(self.layout))
 
 
 _POOL = None

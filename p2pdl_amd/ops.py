@@ -9,6 +9,7 @@ device-resident table of K base pointers (SURVEY.md §8(b) "Ownership").
 from __future__ import annotations
 
 import math
+import threading
 from typing import Iterable, Sequence
 
 import numpy as np
@@ -53,9 +54,10 @@ def _check_f32(t: torch.Tensor, name: str, device) -> None:
 
 
 def pointer_table(tensors: Sequence[torch.Tensor], device) -> torch.Tensor:
-    """Device int64 tensor of data pointers (one small H2D copy)."""
-    host = torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64)
-    return host.to(device, non_blocking=False)
+    """Device int64 tensor of data pointers (one small non-blocking H2D copy
+    through the pinned staging ring)."""
+    host = np.array([t.data_ptr() for t in tensors], dtype=np.int64)
+    return _RING.to_device(host, device).view(torch.int64)
 
 
 def _peer_inputs(peers: Sequence[torch.Tensor], n: int, device):
@@ -143,6 +145,79 @@ _SEG_DTYPE = np.dtype([("peers", "<u8"), ("w", "<u8"), ("out", "<u8"), ("n", "<i
                        ("tile_begin", "<i8")])  # == p2p_segment_t (40 B)
 
 
+class _PinnedRing:
+    """Pinned host staging for the small per-call device tables (segment
+    tables, pointer tables).  The table is written on the host and copied
+    with a non-blocking H2D on the launch stream, so the host can build the
+    next call's table while the GPU still runs this call's kernel (a pageable
+    copy would wait for the stream to drain).  A slot is reused only after
+    the event of the copy that last read it has completed."""
+
+    def __init__(self, slots: int = 8):
+        self.slots = [[None, None] for _ in range(slots)]  # [event, pinned uint8 buffer]
+        self.i = 0
+        self.lock = threading.Lock()
+
+    def to_device(self, host: np.ndarray, dev, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Copy host (uint8-viewable) into `out` (a device uint8 buffer of
+        host.nbytes, allocated here when None) on the current stream."""
+        nbytes = host.nbytes
+        with self.lock:
+            slot = self.slots[self.i % len(self.slots)]
+            self.i += 1
+            if slot[0] is not None:
+                slot[0].synchronize()
+            if slot[1] is None or slot[1].numel() < nbytes:
+                slot[1] = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, pin_memory=True)
+            pinned = slot[1][:nbytes]
+            np.copyto(pinned.numpy(), host.view(np.uint8).reshape(-1))
+            if out is None:
+                out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            with torch.cuda.device(dev):
+                out.copy_(pinned, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            slot[0] = ev
+        return out
+
+
+_RING = _PinnedRing()
+
+
+def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_frac, outs, dev):
+    r = rule_id(rule)
+    if r != P2P_RULE_FEDAVG and K > MAX_ROBUST_PEERS:
+        raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {K}")
+    b = trim_count(K, trim_frac) if (r == P2P_RULE_TRIMMED and trim_b is None) else int(trim_b or 0)
+    tile = int(N.lib().p2p_tile_elems(r, K))
+    L = len(ws)
+    segs = np.zeros(L, dtype=_SEG_DTYPE)
+    n_arr = np.asarray(numels, dtype=np.int64)
+    segs["w"] = [w.data_ptr() for w in ws]
+    if outs is not None:
+        segs["out"] = [o.data_ptr() for o in outs]
+    segs["n"] = n_arr
+    t_arr = -(-n_arr // tile)
+    segs["tile_begin"][1:] = np.cumsum(t_arr)[:-1]
+    tiles = int(t_arr.sum())
+    if tiles == 0:
+        return
+    seg_bytes = segs.nbytes
+    # the table holds device addresses inside itself (segment l -> its row of
+    # K peer pointers): allocate the device buffer first, then fill the host
+    # image with those addresses and copy it once
+    host = np.empty(seg_bytes + ptrs.nbytes, dtype=np.uint8)
+    host[seg_bytes:] = np.ascontiguousarray(ptrs, dtype=np.uint64).view(np.uint8).reshape(-1)
+    buf = torch.empty(host.nbytes, dtype=torch.uint8, device=dev)
+    base = buf.data_ptr()
+    segs["peers"] = np.uint64(base + seg_bytes) + np.arange(L, dtype=np.uint64) * np.uint64(8 * K)
+    host[:seg_bytes] = segs.view(np.uint8)
+    _RING.to_device(host, dev, out=buf)
+    with torch.cuda.device(dev):
+        N.check(N.lib().p2p_aggregate_segments_f32(base, L, tiles, K, r, b, lr, N.stream_handle()),
+                "p2p_aggregate_segments_f32")
+
+
 def aggregate_segments_(ws: Sequence[torch.Tensor], peer_lists: Sequence[Sequence[torch.Tensor]],
                         rule="fedavg", *, lr: float = 0.1, trim_b: int | None = None,
                         trim_frac: float = DEFAULT_TRIM_FRAC,
@@ -159,41 +234,64 @@ def aggregate_segments_(ws: Sequence[torch.Tensor], peer_lists: Sequence[Sequenc
         raise ValueError("need at least one peer update")
     dev = ws[0].device
     N.require_device(ws[0])
-    r = rule_id(rule)
-    if r != P2P_RULE_FEDAVG and K > MAX_ROBUST_PEERS:
-        raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {K}")
-    b = trim_count(K, trim_frac) if (r == P2P_RULE_TRIMMED and trim_b is None) else int(trim_b or 0)
-    tile = int(N.lib().p2p_tile_elems(r, K))
-    segs = np.zeros(L, dtype=_SEG_DTYPE)
-    ptrs = np.zeros((L, K), dtype=np.uint64)
-    tiles = 0
     for l, w in enumerate(ws):
         _check_f32(w, f"w[{l}]", dev)
-        n = w.numel()
-        for j in range(K):
-            p = peer_lists[j][l]
-            _check_f32(p, f"update[{j}][{l}]", dev)
-            if p.numel() != n:
-                raise ValueError(f"update[{j}][{l}] has {p.numel()} elements, expected {n}")
-            ptrs[l, j] = p.data_ptr()
-        segs[l]["w"] = w.data_ptr()
-        segs[l]["out"] = outs[l].data_ptr() if outs is not None else 0
-        segs[l]["n"] = n
-        segs[l]["tile_begin"] = tiles
-        tiles += -(-n // tile)
-    seg_bytes = segs.nbytes
-    buf = torch.empty(seg_bytes + ptrs.nbytes, dtype=torch.uint8, device=dev)
-    base = buf.data_ptr()
-    segs["peers"] = base + seg_bytes + np.arange(L, dtype=np.uint64) * np.uint64(8 * K)
-    host = np.concatenate([segs.view(np.uint8), ptrs.view(np.uint8).reshape(-1)])
-    buf.copy_(torch.from_numpy(host))
-    if tiles == 0:
+    if outs is not None:
+        for l, (o, w) in enumerate(zip(outs, ws)):
+            _check_f32(o, f"out[{l}]", dev)
+            if o.numel() != w.numel():
+                raise ValueError(f"out[{l}] has {o.numel()} elements, expected {w.numel()}")
+    numels = [w.numel() for w in ws]
+    di = dev.index
+    f32 = torch.float32
+    ptrs = np.empty((L, K), dtype=np.uint64)
+    for j, row in enumerate(peer_lists):
+        if len(row) != L:
+            raise ValueError(f"update[{j}] has {len(row)} tensors, expected {L}")
+        # one pass of cheap C getters per tensor; the detailed error (same
+        # checks as _check_f32) only when something is off
+        if not all(t.dtype is f32 and t.get_device() == di and t.is_contiguous() and t.numel() == n
+                   for t, n in zip(row, numels)):
+            for l, (t, n) in enumerate(zip(row, numels)):
+                _check_f32(t, f"update[{j}][{l}]", dev)
+                if t.numel() != n:
+                    raise ValueError(f"update[{j}][{l}] has {t.numel()} elements, expected {n}")
+        ptrs[:, j] = [t.data_ptr() for t in row]
+    _launch_segments(ws, ptrs, numels, rule, K, lr, trim_b, trim_frac, outs, dev)
+
+
+def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: Sequence[int],
+                         offsets: Sequence[int], rule="fedavg", *, lr: float = 0.1,
+                         trim_b: int | None = None, trim_frac: float = DEFAULT_TRIM_FRAC) -> None:
+    """aggregate_segments_ for updates that are rows of one [K_max, N] fp32
+    slab (what node.inbox.DeviceInbox lands): update j's tensor for key l is
+    slab[rows[j], offsets[l] : offsets[l] + ws[l].numel()].  The (L, K) peer
+    table is computed with one broadcast instead of inspecting L*K tensors."""
+    L, K = len(ws), len(rows)
+    if L == 0:
         return
-    with torch.cuda.device(dev):
-        N.check(N.lib().p2p_aggregate_segments_f32(base, L, tiles, K, r, b, lr, N.stream_handle()),
-                "p2p_aggregate_segments_f32")
-    # keep the table alive until the kernel has consumed it (stream-ordered reuse)
-    buf.record_stream(torch.cuda.current_stream(dev))
+    if K == 0:
+        raise ValueError("need at least one peer update")
+    dev = ws[0].device
+    N.require_device(ws[0])
+    _check_f32(slab, "slab", dev)
+    if slab.dim() != 2:
+        raise ValueError("slab must be [K_max, N]")
+    numels = []
+    for l, w in enumerate(ws):
+        _check_f32(w, f"w[{l}]", dev)
+        numels.append(w.numel())
+    rows_a = np.asarray(rows, dtype=np.int64)
+    offs_a = np.asarray(offsets, dtype=np.int64)
+    kmax, width = slab.shape
+    if rows_a.min() < 0 or rows_a.max() >= kmax:
+        raise IndexError("slab row out of range")
+    if offs_a.min() < 0 or (offs_a + np.asarray(numels, dtype=np.int64)).max() > width:
+        raise IndexError("segment outside the slab row")
+    base, stride = slab.data_ptr(), slab.stride(0) * 4
+    ptrs = (np.uint64(base) + rows_a.astype(np.uint64)[None, :] * np.uint64(stride)
+            + offs_a.astype(np.uint64)[:, None] * np.uint64(4))
+    _launch_segments(ws, ptrs, numels, rule, K, lr, trim_b, trim_frac, None, dev)
 
 
 # ------------------------------------------------------------------ K4
@@ -236,7 +334,7 @@ def delta_snapshot_segments_(curs: Sequence[torch.Tensor], prevs: Sequence[torch
         tiles += -(-c.numel() // DELTA_TILE)
     if tiles == 0:
         return
-    buf = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
+    buf = _RING.to_device(segs.view(np.uint8), dev)
     with torch.cuda.device(dev):
         N.check(N.lib().p2p_delta_snapshot_segments_f32(buf.data_ptr(), L, tiles, int(first), N.stream_handle()),
                 "p2p_delta_snapshot_segments_f32")
@@ -255,8 +353,9 @@ def sha256_batch_device(msgs: torch.Tensor, offsets: Sequence[int], lengths: Seq
     if K == 0:
         return digests[:0]
     base = msgs.data_ptr()
-    ptrs = torch.tensor([base + int(o) for o in offsets], dtype=torch.int64).to(dev)
-    lens = torch.tensor([int(x) for x in lengths], dtype=torch.int64).to(dev)
+    tab = _RING.to_device(np.array([[base + int(o) for o in offsets], [int(x) for x in lengths]],
+                                   dtype=np.int64), dev).view(torch.int64)
+    ptrs, lens = tab[:K], tab[K:]
     with torch.cuda.device(dev):
         N.check(N.lib().p2p_sha256_batch(ptrs.data_ptr(), lens.data_ptr(), K, digests.data_ptr(),
                                          N.stream_handle()), "p2p_sha256_batch")

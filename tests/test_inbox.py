@@ -366,3 +366,64 @@ def test_device_inbox_concurrent_landing(cuda):
         ref = pickle.loads(ser[j])
         for key in ref:
             assert_bits_equal(got[j][key].cpu().numpy(), ref[key].numpy(), what=f"update {j} {key}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule", ["fedavg", "median", "trimmed"])
+def test_landed_updates_take_the_slab_fast_path(cuda, rule, monkeypatch):
+    """aggregate_models on DeviceInbox-landed updates builds its kernel table
+    from (slab, rows, key offsets) -- no per-tensor work -- and gives the same
+    bits as the general path and the oracle; one plain dict among them sends
+    the call down the general path."""
+    from p2pdl_amd import ops
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
+    k = 7
+    template = {name: torch.zeros(s, device=cuda) for name, s in MLP_SHAPES}
+    inbox = DeviceInbox(template, k_max=k, device=cuda)
+    ser = [pickle.dumps(mlp_update(60 + j)) for j in range(k)]
+    landed = [inbox.land(s) for s in ser]
+    n = sum(int(np.prod(s)) for _, s in MLP_SHAPES)
+    w = oracle.synth(n, 5, 0xFFFFF, 5e-2)
+    flat = [np.concatenate([pickle.loads(s)[name].numpy().reshape(-1) for name, _ in MLP_SHAPES]) for s in ser]
+    if rule == "fedavg":
+        want, _ = oracle.fedavg(flat, w)
+    else:
+        r = ops.rule_id(rule)
+        want, _ = oracle.robust(flat, r, ops.trim_count(k) if r == 2 else 0, w=w)
+
+    def run(updates):
+        model = torch.nn.Module()
+        offs = 0
+        for name, s in MLP_SHAPES:
+            m = int(np.prod(s))
+            mod, attr = name.split(".")
+            if not hasattr(model, mod):
+                model.add_module(mod, torch.nn.Module())
+            getattr(model, mod).register_parameter(attr, torch.nn.Parameter(
+                torch.from_numpy(w[offs:offs + m].reshape(s).copy()).to(cuda)))
+            offs += m
+        node = types.SimpleNamespace(model=model, trainers_list=[0] * k, addr="a", port=1, neighbors=[],
+                                     received_models=[{"model": u, "sender": j} for j, u in enumerate(updates)])
+        agg.aggregate_models(node, rule=rule)
+        assert node.received_models == []
+        return np.concatenate([t.detach().cpu().numpy().reshape(-1) for t in model.state_dict().values()])
+
+    def boom(*a, **kw):
+        raise AssertionError("wrong path")
+
+    with monkeypatch.context() as m:
+        m.setattr(ops, "aggregate_segments_", boom)  # must not be reached
+        assert_bits_equal(run(landed), want, what=f"fast path {rule}")
+    with monkeypatch.context() as m:
+        m.setattr(ops, "aggregate_slab_rows_", boom)
+        mixed = landed[:-1] + [dict(landed[-1])]  # a plain dict: general path
+        assert_bits_equal(run(mixed), want, what=f"general path {rule}")
+    with pytest.raises(TypeError):
+        landed[0]["fc1.weight"] = torch.zeros(1)
+    with pytest.raises(TypeError):
+        del landed[0]["fc1.bias"]
+    back = pickle.loads(pickle.dumps(landed[0]))  # copies, not the slab
+    assert type(back) is collections.OrderedDict and list(back) == list(landed[0])
+    assert back["fc3.bias"].untyped_storage().nbytes() == 10 * 4
