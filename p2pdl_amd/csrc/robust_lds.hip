@@ -50,7 +50,8 @@ __device__ __forceinline__ u16x2 pmax(u16x2 a, u16x2 b) { return __builtin_eleme
 #define P2P_LDS __attribute__((address_space(3)))
 
 // Diagnostic builds only (make diag): 1 = no DMA (sort stale LDS: compute
-// time), 2 = no sort (DMA + barriers + stores: staging time).  Wrong results.
+// time), 2 = no sort (DMA + barriers + stores: staging time), 3 = trimmed
+// mean without the rank-ordered sum (sort + staging).  Wrong results.
 #ifndef P2P_LDS_DIAG
 #define P2P_LDS_DIAG 0
 #endif
@@ -73,6 +74,22 @@ __device__ __forceinline__ uint32_t xq(uint32_t x) {
   static_assert(M >= 1 && M <= 3, "quad partner");
   return dpp<M == 1 ? 0xB1 : (M == 2 ? 0x4E : 0x1B)>(x);
 }
+template <int M>
+__device__ __forceinline__ fk xq(fk x) {
+  return fk{__uint_as_float(xq<M>(__float_as_uint(x.x)))};
+}
+
+// Type-generic pieces of the L-lane reduction: uint32 total-order keys or
+// float values (NaN-free waves, robust_nets.h).  keep(a, p, hi) is
+// min(a, p) / max(a, p) in ONE v_med3 against a lane-constant 0 / ~0 (keys)
+// or -inf / +inf (floats); value() is the float the element stands for.
+__device__ __forceinline__ uint32_t keep(uint32_t a, uint32_t p, uint32_t lim) { return umed3(a, p, lim); }
+__device__ __forceinline__ fk keep(fk a, fk p, fk lim) { return fk{__builtin_amdgcn_fmed3f(a.x, p.x, lim.x)}; }
+__device__ __forceinline__ uint32_t keep_limit(uint32_t, bool hi) { return hi ? 0xFFFFFFFFu : 0u; }
+__device__ __forceinline__ fk keep_limit(fk, bool hi) { return fk{hi ? __builtin_inff() : -__builtin_inff()}; }
+__device__ __forceinline__ float value(uint32_t k) { return __uint_as_float(key2f(k)); }
+__device__ __forceinline__ float value(fk f) { return f.x; }
+
 // value of slice q-1 of the same coordinate (slice 0 receives its own)
 template <int L>
 __device__ __forceinline__ float from_prev_slice(float x) {
@@ -125,34 +142,34 @@ __device__ __forceinline__ TileSrc locate(const float* const* peers, const Seg* 
   }
 }
 
-// The L-lane reduction of one coordinate.  v[] holds this lane's H keys
-// (pads = 0xFFFFFFFF); returns the aggregate, valid in the lane where
-// `own` is set on return.
-template <int L, int H, int RULE, int MODE>
-__device__ __forceinline__ float reduce_keys(uint32_t (&v)[H], int q, int K, int trim_b, bool& own) {
+// The L-lane reduction of one coordinate.  v[] holds this lane's H elements
+// (uint32 keys, pads 0xFFFFFFFF; or float values, pads +inf); returns the
+// aggregate, valid in the lane where `own` is set on return.
+template <int L, int H, int RULE, int MODE, typename T>
+__device__ __forceinline__ float reduce_keys(T (&v)[H], int q, int K, int trim_b, bool& own) {
   static_assert(L == 1 || L == 2 || L == 4, "lanes per coordinate");
   if constexpr (L == 1) {
     if constexpr (MODE == 0) sort_full<H>(v); else run_special<H, MODE>(v);
     own = true;
     if constexpr (RULE == P2P_RULE_MEDIAN) {
-      if constexpr (MODE == 1) return __uint_as_float(key2f(v[(H - 1) / 2]));
+      if constexpr (MODE == 1) return value(v[(H - 1) / 2]);
       const int r = (K - 1) / 2;
-      uint32_t sel = v[0];
+      T sel = v[0];
 #pragma unroll
       for (int j = 1; j < H; ++j) sel = (j == r) ? v[j] : sel;
-      return __uint_as_float(key2f(sel));
+      return value(sel);
     } else {
       float acc = 0.f;
       if constexpr (MODE == 2) {
         constexpr int b = (H * 2) / 10;
 #pragma unroll
-        for (int j = b; j < H - b; ++j) acc = __fadd_rn(acc, __uint_as_float(key2f(v[j])));
+        for (int j = b; j < H - b; ++j) acc = __fadd_rn(acc, value(v[j]));
         return acc / static_cast<float>(H - 2 * b);
       }
       const int hi = K - trim_b;
 #pragma unroll
       for (int j = 0; j < H; ++j)
-        if (j >= trim_b && j < hi) acc = __fadd_rn(acc, __uint_as_float(key2f(v[j])));  // uniform predicate
+        if (j >= trim_b && j < hi) acc = __fadd_rn(acc, value(v[j]));  // uniform predicate
       return acc / static_cast<float>(K - 2 * trim_b);
     }
   } else {
@@ -160,31 +177,31 @@ __device__ __forceinline__ float reduce_keys(uint32_t (&v)[H], int q, int K, int
 #pragma unroll
     for (int s = 2; s <= L; s *= 2) {
       {  // flip against the mirrored lane of the s-lane group
-        const uint32_t keep = (q & (s / 2)) ? 0xFFFFFFFFu : 0u;
+        const T lim = keep_limit(v[0], (q & (s / 2)) != 0);
 #pragma unroll
         for (int j = 0; j < H / 2; ++j) {
-          const uint32_t a = v[j], b = v[H - 1 - j];
-          const uint32_t pa = (s == 2) ? xq<1>(b) : xq<3>(b);  // partner's v[H-1-j]
-          const uint32_t pb = (s == 2) ? xq<1>(a) : xq<3>(a);  // partner's v[j]
-          v[j] = umed3(a, pa, keep);
-          v[H - 1 - j] = umed3(b, pb, keep);
+          const T a = v[j], b = v[H - 1 - j];
+          const T pa = (s == 2) ? xq<1>(b) : xq<3>(b);  // partner's v[H-1-j]
+          const T pb = (s == 2) ? xq<1>(a) : xq<3>(a);  // partner's v[j]
+          v[j] = keep(a, pa, lim);
+          v[H - 1 - j] = keep(b, pb, lim);
         }
       }
       if constexpr (RULE == P2P_RULE_MEDIAN && MODE == 1) {
         if (s == L) {  // slices q < L/2 now hold the K/2 smallest keys; median = their max
-          uint32_t mx = v[0];
+          T mx = v[0];
 #pragma unroll
           for (int j = 1; j < H; ++j) mx = max(mx, v[j]);
           if constexpr (L == 4) mx = max(mx, xq<1>(mx));
           own = (q == 0);
-          return __uint_as_float(key2f(mx));
+          return value(mx);
         }
       }
 #pragma unroll
       for (int d = s / 4; d >= 1; d /= 2) {  // half-cleaners (only at s = 4: d = 1)
-        const uint32_t keep = (q & d) ? 0xFFFFFFFFu : 0u;
+        const T lim = keep_limit(v[0], (q & d) != 0);
 #pragma unroll
-        for (int j = 0; j < H; ++j) v[j] = umed3(v[j], xq<1>(v[j]), keep);
+        for (int j = 0; j < H; ++j) v[j] = keep(v[j], xq<1>(v[j]), lim);
       }
       bmerge<H>(v);
     }
@@ -192,20 +209,26 @@ __device__ __forceinline__ float reduce_keys(uint32_t (&v)[H], int q, int K, int
     if constexpr (RULE == P2P_RULE_MEDIAN) {
       const int r = (K - 1) / 2;
       const int rl = r % H;
-      uint32_t sel = v[0];
+      T sel = v[0];
 #pragma unroll
       for (int j = 1; j < H; ++j) sel = (j == rl) ? v[j] : sel;
       own = (q == r / H);
-      return __uint_as_float(key2f(sel));
+      return value(sel);
     } else {
+      if constexpr (P2P_LDS_DIAG == 3) {  // diag: no sum (keep the sort live)
+        uint32_t x = __float_as_uint(value(v[0]));
+#pragma unroll
+        for (int j = 1; j < H; ++j) x ^= __float_as_uint(value(v[j]));
+        own = (q == L - 1);
+        return __uint_as_float(x);
+      }
       // ascending-rank sequential sum from +0: slice 0's ranks, then slice 1 ...
       constexpr int KP = L * H;
       const int b = MODE == 2 ? (KP * 2) / 10 : trim_b;
       const int hi = MODE == 2 ? KP - b : K - trim_b;
-      if constexpr (MODE == 2) {  // once: a key is summed in up to L phases
+      float f[H];
 #pragma unroll
-        for (int j = 0; j < H; ++j) v[j] = key2f(v[j]);
-      }
+      for (int j = 0; j < H; ++j) f[j] = value(v[j]);  // once: a value is summed in up to L phases
       float acc = 0.f;
 #pragma unroll
       for (int p = 0; p < L; ++p) {
@@ -214,7 +237,7 @@ __device__ __forceinline__ float reduce_keys(uint32_t (&v)[H], int q, int K, int
         for (int j = 0; j < H; ++j) {
           const int g = p * H + j;
           if (g >= b && g < hi)  // wave-uniform
-            a = __fadd_rn(a, __uint_as_float(MODE == 2 ? v[j] : key2f(v[j])));
+            a = __fadd_rn(a, f[j]);
         }
         acc = (q == p) ? a : acc;
       }
@@ -227,15 +250,20 @@ __device__ __forceinline__ float reduce_keys(uint32_t (&v)[H], int q, int K, int
 // ---- two-pass radix median, K = 256 (layout "radix16", PK = 2) -------------
 // Two coordinates per lane group: lane 4c+q holds keys 64q..64q+63 of
 // coordinates c (ka) and c+16 (kb).  Pass 1 runs the L = 4 median chain on
-// packed u16x2 keys -- the hi16 halves of both coordinates in one VGPR --
-// because v_pk_min/max_u16 sort two keys per half-rate instruction
-// (profiles/r01/probes: 0.61x the VALU time per coordinate of the uint32
-// chain).  It yields mh = hi16 of the rank-127 key and the rank-126 hi16.
-// When rank 126's hi16 < mh, exactly 127 keys lie below mh's bucket, so the
-// median is the SMALLEST key whose hi16 is mh: one min over (key - mh<<16)
-// (keys below the bucket wrap above 2^16, keys above it are >= 2^16).
-// Otherwise (a tie of hi16 across ranks 126/127 anywhere in the wave) the
-// wave runs the exact uint32 chain on both coordinates.
+// packed u16x2 keys -- a 16-bit image of both coordinates' keys in one VGPR --
+// because v_pk_min/max_u16 sort two keys per half-rate instruction.  The
+// 16-bit image is a per-coordinate AFFINE map of the uint32 key,
+//   k16 = sat16(sat_sub(key, base) >> s),
+// with base / s from the min / max of 32 sampled keys (8 per lane), so the
+// 65536 buckets span the data's actual range (round 1's hi16-of-the-raw-key
+// image put ~86% of waves on the fallback: the median's neighbours shared a
+// bucket).  The map is monotone (non-decreasing), so the rank-127 bucket mh
+// holds the median; pass 1 also yields the rank-126 bucket.  When rank 126's
+// bucket < mh, exactly 127 keys lie below mh's bucket and the median is the
+// SMALLEST key >= lo = base + (mh << s): one min over (key - lo) (keys below
+// lo wrap above every key >= lo).  Otherwise -- a tie across ranks 126/127,
+// or mh saturated at 0 / 65535 -- the wave runs the exact uint32 chain on
+// both coordinates.
 __device__ __forceinline__ uint32_t pbits(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 __device__ __forceinline__ u16x2 pvec(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 template <int M>
@@ -245,11 +273,44 @@ __device__ __forceinline__ u16x2 pkeep(u16x2 a, u16x2 pa, bool hi) {
   return hi ? h : lo;
 }
 
+#ifdef P2P_LAB
+__device__ int g_lab_fallback[64];  // lab builds only: waves that took the exact fallback
+#endif
+
+// base / shift of the affine 16-bit map from the quad's 32 sampled keys
+// (this lane's keys 0..7): every key in [min, max] of the sample maps without
+// saturation, the rest saturates to 0 / 65535 (still monotone).
+__device__ __forceinline__ void affine_params(const uint32_t (&k)[64], uint32_t& base, uint32_t& s) {
+  uint32_t lo = k[0], hi = k[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) {
+    lo = min(lo, k[j]);
+    hi = max(hi, k[j]);
+  }
+  lo = min(lo, xq<1>(lo));
+  hi = max(hi, xq<1>(hi));
+  lo = min(lo, xq<2>(lo));
+  hi = max(hi, xq<2>(hi));
+  const uint32_t range = hi - lo;
+  const uint32_t bits = range ? 32u - static_cast<uint32_t>(__builtin_clz(range)) : 0u;
+  base = lo;
+  s = bits > 16u ? bits - 16u : 0u;
+}
+
+__device__ __forceinline__ uint32_t affine16(uint32_t key, uint32_t base, uint32_t s) {
+  return __builtin_elementwise_sub_sat(key, base) >> s;  // saturated to 16 bits by the pack
+}
+
 __device__ __forceinline__ void radix_median_pair(uint32_t (&ka)[64], uint32_t (&kb)[64], int q, float& ra,
                                                   float& rb) {
+  uint32_t base_a, s_a, base_b, s_b;
+  affine_params(ka, base_a, s_a);
+  affine_params(kb, base_b, s_b);
   u16x2 h[64];
 #pragma unroll
-  for (int j = 0; j < 64; ++j) h[j] = pvec((ka[j] >> 16) | (kb[j] & 0xFFFF0000u));
+  for (int j = 0; j < 64; ++j)  // v_cvt_pk_u16_u32: two u32 -> u16x2, each saturated at 0xFFFF
+    h[j] = __builtin_amdgcn_cvt_pk_u16(static_cast<int>(affine16(ka[j], base_a, s_a)),
+                                       static_cast<int>(affine16(kb[j], base_b, s_b)));
   sort_full<64>(h);  // the generated networks are type-generic (min / max below)
   const bool k1 = q & 1, k2 = q & 2;
 #pragma unroll
@@ -265,8 +326,8 @@ __device__ __forceinline__ void radix_median_pair(uint32_t (&ka)[64], uint32_t (
     h[j] = pkeep(a, pxq<3>(b), k2);
     h[63 - j] = pkeep(b, pxq<3>(a), k2);
   }
-  // lanes q < 2 now hold the 128 smallest hi16 of each coordinate: the
-  // largest two of them are ranks 127 and 126
+  // lanes q < 2 now hold the 128 smallest 16-bit keys of each coordinate:
+  // the largest two of them are ranks 127 and 126
   u16x2 m1 = h[0], m2 = pvec(0u);
 #pragma unroll
   for (int j = 1; j < 64; ++j) {
@@ -280,22 +341,25 @@ __device__ __forceinline__ void radix_median_pair(uint32_t (&ka)[64], uint32_t (
   }
   const uint32_t mh = dpp<0x00>(pbits(m1)), sh = dpp<0x00>(pbits(m2));  // lane 4c's values to its quad
   const uint32_t mha = mh & 0xFFFFu, mhb = mh >> 16;
-  const bool fast = (sh & 0xFFFFu) < mha && (sh >> 16) < mhb;
+  const bool fast = (sh & 0xFFFFu) < mha && (sh >> 16) < mhb && mha != 0xFFFFu && mhb != 0xFFFFu;
   if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
-    const uint32_t ba = mha << 16, bb = mhb << 16;
+    const uint32_t la = base_a + (mha << s_a), lb = base_b + (mhb << s_b);  // smallest key of bucket mh
     uint32_t ua = 0xFFFFFFFFu, ub = 0xFFFFFFFFu;
 #pragma unroll
     for (int j = 0; j < 64; ++j) {
-      ua = min(ua, ka[j] - ba);
-      ub = min(ub, kb[j] - bb);
+      ua = min(ua, ka[j] - la);
+      ub = min(ub, kb[j] - lb);
     }
     ua = min(ua, xq<1>(ua));
     ub = min(ub, xq<1>(ub));
     ua = min(ua, xq<2>(ua));
     ub = min(ub, xq<2>(ub));
-    ra = __uint_as_float(key2f(ua + ba));
-    rb = __uint_as_float(key2f(ub + bb));
+    ra = __uint_as_float(key2f(ua + la));
+    rb = __uint_as_float(key2f(ub + lb));
   } else {  // valid in lane q == 0 either way
+#ifdef P2P_LAB
+    atomicAdd(&g_lab_fallback[threadIdx.x & 63], 1);  // per-lane slots: a vector atomic
+#endif
     bool own = false;
     ra = reduce_keys<4, 64, P2P_RULE_MEDIAN, 1>(ka, q, 256, 0, own);
     rb = reduce_keys<4, 64, P2P_RULE_MEDIAN, 1>(kb, q, 256, 0, own);
@@ -535,11 +599,6 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
     }
     block_sync_lds();  // B: image consumed, free for the DMA D tiles ahead
     advance(t);
-#pragma unroll
-    for (int j = 0; j < H; ++j) {
-      const bool real = (MODE != 0) || (q * H + j < K);
-      v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pads sort after every real key
-    }
     bool own = false;
     float agg;
     if constexpr (P2P_LDS_DIAG == 2) {
@@ -549,7 +608,21 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
       agg = __uint_as_float(x);
       own = q == 0;
     } else {
-      agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
+      bool fast = false;  // every slot real (K == KP) and no NaN in the wave: the float network
+      if constexpr (MODE != 0) fast = !wave_has_nan(v);
+      if (fast) {
+        fk f[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) f[j].x = __uint_as_float(v[j]);
+        agg = reduce_keys<L, H, RULE, MODE>(f, q, K, trim_b, own);
+      } else {
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+          const bool real = (MODE != 0) || (q * H + j < K);
+          v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pads sort after every real key
+        }
+        agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
+      }
     }
     if (own && i < me.n) {
       if (me.out) stg(me.out + i, agg);

@@ -7,6 +7,41 @@
 
 namespace p2p {
 
+// NaN-free fast path: the networks run on the float values themselves.
+// v_min / v_max / v_med3_f32 order -0 < +0 and keep denormals and +-inf
+// exactly as the uint32 total-order keys do (tools/fminmax_probe.hip,
+// profiles/r01/probes), so for NaN-free inputs every rank -- and every bit of
+// the selected value -- is the same as the key network's, without the key map
+// (2 VALU per key in, 2 per key out).  robust.hip / robust_lds.hip are built
+// with -mno-amdgpu-ieee -fno-honor-nans, so min / max need no canonicalising
+// v_max_f32 x,x per input; the NaN test is therefore an explicit vector
+// compare (the compiler would fold isnan away) and a wave with any NaN takes
+// the uint32-key network.
+struct fk {
+  float x;
+};
+using ::max;  // keep the global (integer / packed) overloads visible next to fk's
+using ::min;
+__device__ __forceinline__ fk min(fk a, fk b) { return fk{__builtin_fminf(a.x, b.x)}; }
+__device__ __forceinline__ fk max(fk a, fk b) { return fk{__builtin_fmaxf(a.x, b.x)}; }
+
+// Lanes of the wave for which a or b is NaN (v_cmp_u_f32 into an SGPR pair).
+__device__ __forceinline__ uint64_t unordered_mask(float a, float b) {
+  uint64_t m;
+  asm volatile("v_cmp_u_f32 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b));
+  return m;
+}
+
+// Any NaN among the n values of any lane of the wave (wave-uniform).
+template <int N>
+__device__ __forceinline__ bool wave_has_nan(const uint32_t (&bits)[N]) {
+  static_assert(N % 2 == 0, "pairs");
+  uint64_t m = 0;
+#pragma unroll
+  for (int j = 0; j < N / 2; ++j) m |= unordered_mask(__uint_as_float(bits[j]), __uint_as_float(bits[j + N / 2]));
+  return m != 0;
+}
+
 template <bool ASC, typename T>
 __device__ __forceinline__ void ce(T& a, T& b) {
   const T lo = min(a, b), hi = max(a, b);
@@ -33,7 +68,8 @@ template <int KP, bool ASC = true, typename T> __device__ __forceinline__ void s
 // Sorts a bitonic sequence of KP keys ascending (half-cleaners n/2 .. 1).
 template <int KP, typename T> __device__ __forceinline__ void bmerge(T (&v)[KP]) {
   if constexpr (KP == 32) net_bmerge32<true>(v);
-  else net_bmerge64<true>(v);
+  else if constexpr (KP == 64) net_bmerge64<true>(v);
+  else net_bmerge128<true>(v);
 }
 
 // MODE 0: generic (full sort + runtime rank / trim);

@@ -353,6 +353,49 @@ def test_robust_segments(cuda, rule, k):
     assert_bits_equal(got, w_ref, what=f"segments {rule} K={k}")
 
 
+def nan_free_special_peers(k, n, seed):
+    """Every value class the float fast path must order exactly like the
+    uint32 keys -- -0 / +0, denormals of both signs, +-inf, the largest
+    finite values, heavy ties -- and no NaN, so NaN-free waves take the float
+    network (robust_nets.h)."""
+    rng = np.random.default_rng(seed)
+    sp = np.array([0.0, -0.0, 1e-45, -1e-45, 3e-39, -3e-39, np.inf, -np.inf, 3.4e38, -3.4e38,
+                   1.0, -1.0, 0.5], dtype=np.float32)
+    peers = []
+    with np.errstate(all="raise"):
+        for p in range(k):
+            x = oracle.synth(n, seed, p, 1e-2)
+            x[: n // 4] = np.where(rng.random(n // 4) < 0.5, np.float32(-0.0), np.float32(0.0))
+            q = slice(n // 4, n // 2)
+            x[q] = np.round(x[q] * 2 ** 5) / 2 ** 5  # ties
+            m = rng.random(n) < 0.2
+            x[m] = rng.choice(sp, size=int(m.sum()))
+            peers.append(x.astype(np.float32))
+    return peers
+
+
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+@pytest.mark.parametrize("k", [64, 128, 256])
+@pytest.mark.parametrize("nan_stripe", [False, True])
+def test_robust_float_fast_path_specials(cuda, rule, k, nan_stripe):
+    """K == KP with b = floor(0.2 K): NaN-free waves run the float network,
+    a wave holding one NaN runs the uint32-key network; both bit-exact with
+    the oracle (median: the selected bits, so -0 vs +0 included)."""
+    n = 40_003
+    peers = nan_free_special_peers(k, n, 13 * k + int(nan_stripe))
+    if nan_stripe:  # one NaN in every 997th coordinate: those waves take the key path
+        for p in range(0, k, 11):
+            peers[p][::997] = np.float32(np.nan) if p % 2 else np.float32(-np.nan)
+    w = oracle.synth(n, 4, 0xFFFFF, 5e-2)
+    r = ops.rule_id(rule)
+    b = ops.trim_count(k) if rule == "trimmed" else 0
+    w_ref, out_ref = oracle.robust(peers, r, b, w=w)
+    wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate([to_dev(p, cuda) for p in peers], rule, w=wt, out=out, trim_b=b)
+    assert_bits_equal(host(out), out_ref, nan_equal=(rule != "median"), what=f"{rule} K={k} nan={nan_stripe}")
+    assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k} nan={nan_stripe}")
+
+
 @pytest.mark.parametrize("k,b", [(5, 0), (5, 2), (10, 3), (128, 0), (128, 63), (200, 10), (256, 51), (256, 100)])
 def test_trimmed_explicit_b(cuda, k, b):
     n = 1000
