@@ -275,69 +275,87 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
 
 
 # ------------------------------------------------------------------ cfg3 full job
-def measure_cfg3_full(c: Ctx, args, passes=2):
-    """The fixed cfg3 job: 1B coordinates x 256 peers in eight 125M tiles;
-    rank r runs tiles r, r+N, ... (8/N of them).  Per tile: regenerate the
-    tile's 256 peer slices (+ its w slice) outside the timed region, run the
-    FedAvg kernel (HIP events), then at N > 1 all-gather the tile round into
-    the global model (events on the comm stream).  Reported time = sum of
-    tile kernel times + sum of all-gather times, max over ranks."""
+def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
+    """The fixed cfg3 job: 1B coordinates x 256 peers (1.02 TB of peer data).
+    Ownership is round-robin by chunk of C = 15.625M coordinates (global
+    chunk g belongs to rank g mod N, as p2pdl_amd.sharded plans it), and each
+    rank works through its 64/N chunks in tiles of 8 chunks (125M
+    coordinates, 128 GB of peer slices -- 1.02 TB does not fit 288 GB).  Per
+    tile: regenerate the tile's 256 peer slices and w slice OUTSIDE the timed
+    region, then reduce chunk by chunk on the compute stream while the
+    all-gather of chunk s (RCCL over xGMI) runs on a second stream beside
+    chunk s+1.  Reported time = sum over tiles of (first kernel start -> last
+    all-gather end), max over ranks; the serial kernel and all-gather sums are
+    reported beside it."""
     world, rank, dev = c.world, c.rank, c.dev
     K, seed, T = 256, WORKLOADS["cfg3"][3], CFG3_TILE
-    ntiles = CFG3_COORDS // T
-    if ntiles % world:
-        raise SystemExit(f"cfg3-full: {ntiles} tiles do not split over {world} GPUs")
-    per = ntiles // world
+    C = T // chunks
+    nchunks = CFG3_COORDS // C
+    if nchunks % (world * chunks):
+        raise SystemExit(f"cfg3-full: {nchunks} chunks do not split into tiles of {chunks} over {world} GPUs")
+    per = nchunks // (world * chunks)  # tiles per rank
     slab = torch.empty((K, T), dtype=torch.float32, device=dev)
     w = torch.empty(T, dtype=torch.float32, device=dev)
     w_full = torch.empty(CFG3_COORDS, dtype=torch.float32, device=dev) if world > 1 else None
-    table = ops.pointer_table(list(slab), dev)
+    tables = [ops.pointer_table([slab[p, s * C:(s + 1) * C] for p in range(K)], dev) for s in range(chunks)]
     comp = torch.cuda.current_stream(dev)
     comm = torch.cuda.Stream(dev)
-    kern_ms, gather_ms = [], []
+    wall, kern, gath = [], [], []
     checked = False
     for _ in range(passes):
-        k_tot = g_tot = 0.0
-        for s in range(per):
-            tile = s * world + rank  # round s: global tile s*N + r (contiguous round in the global model)
+        w_tot = k_tot = g_tot = 0.0
+        for u in range(per):
+            # local chunk s of tile u is global chunk (u*chunks + s)*N + rank: in the
+            # synthetic generator that is "rank" r + u*chunks*N of an N-rank chunk map
+            vr = rank + u * chunks * world
             for p in range(K):
-                ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE, T, ntiles, tile)
-            ops.fill_synthetic_(w, seed, W_PEER, W_SCALE, T, ntiles, tile)
+                ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE, C, world, vr)
+            ops.fill_synthetic_(w, seed, W_PEER, W_SCALE, C, world, vr)
+            torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-            e[0].record(comp)
-            ops.aggregate(None, "fedavg", w=w, lr=0.1, table=table)
-            e[1].record(comp)
-            if world > 1:
-                comm.wait_event(e[1])
-                with torch.cuda.stream(comm):
-                    e[2].record(comm)
-                    dist.all_gather_into_tensor(w_full[s * world * T:(s + 1) * world * T], w)
-                    e[3].record(comm)
-                comp.wait_stream(comm)
+            ev = []
+            start = torch.cuda.Event(enable_timing=True)
+            start.record(comp)
+            for s in range(chunks):
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                e[0].record(comp)
+                ops.aggregate(None, "fedavg", w=w[s * C:(s + 1) * C], lr=0.1, table=tables[s])
+                e[1].record(comp)
+                if world > 1:
+                    comm.wait_event(e[1])
+                    g0 = ((u * chunks + s) * world) * C
+                    with torch.cuda.stream(comm):
+                        e[2].record(comm)
+                        dist.all_gather_into_tensor(w_full[g0:g0 + world * C], w[s * C:(s + 1) * C])
+                        e[3].record(comm)
+                ev.append(e)
+            comp.wait_stream(comm)
+            end = torch.cuda.Event(enable_timing=True)
+            end.record(comp)
             torch.cuda.synchronize()
-            k_tot += e[0].elapsed_time(e[1])
+            w_tot += start.elapsed_time(end)
+            k_tot += sum(e[0].elapsed_time(e[1]) for e in ev)
             if world > 1:
-                g_tot += e[2].elapsed_time(e[3])
+                g_tot += sum(e[2].elapsed_time(e[3]) for e in ev)
             if not checked and not args.no_check and rank == 0:
                 m = 4096
-                got = (w_full[s * world * T:s * world * T + m] if world > 1 else w[:m]).cpu().numpy()
-                ok = bits_equal(got, oracle_expect("fedavg", K, m, seed, T, ntiles, s * world))
-                log(f"[rank 0] cfg3-full: spot check of tile {s * world} vs oracle: {'bit-exact' if ok else 'MISMATCH'}")
+                got = (w_full[:m] if world > 1 else w[:m]).cpu().numpy()  # global chunk 0: rank 0, tile 0
+                ok = bits_equal(got, oracle_expect("fedavg", K, m, seed, C, world, 0))
+                log(f"[rank 0] cfg3-full: spot check of global chunk 0 vs oracle: {'bit-exact' if ok else 'MISMATCH'}")
                 if not ok:
                     raise SystemExit("bench: cfg3-full differs from the oracle")
                 checked = True
-        kern_ms.append(k_tot)
-        gather_ms.append(g_tot)
-    k_ms, g_ms = min(kern_ms), min(gather_ms)  # best pass (each pass is the whole job)
+        wall.append(w_tot)
+        kern.append(k_tot)
+        gath.append(g_tot)
+    best = min(range(passes), key=lambda i: wall[i])  # best pass (each pass is the whole job)
+    tot, k_ms, g_ms = wall[best], kern[best], gath[best]
     if world > 1:
-        t = torch.tensor([k_ms + g_ms, k_ms, g_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([tot, k_ms, g_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         tot, k_ms, g_ms = (float(x) for x in t.tolist())
-    else:
-        tot = k_ms
-    del slab, w, w_full, table
+    del slab, w, w_full, tables
     torch.cuda.empty_cache()
     peer_bytes = K * CFG3_COORDS * 4
     return {
@@ -345,11 +363,12 @@ def measure_cfg3_full(c: Ctx, args, passes=2):
         "ms_per_job": round(tot, 3), "kernel_ms_sum": round(k_ms, 3), "allgather_ms_sum": round(g_ms, 3),
         "scaling": "strong", "dtype": "fp32",
         "config": {"workload": f"cfg3 full job: fedavg over {K} peers x {CFG3_COORDS:,} fp32 coords "
-                               f"({peer_bytes/1e12:.3f} TB) as {ntiles} tiles of {T:,}; {per} tile(s) per GPU",
-                   "tiles_per_gpu": per, "parallelism": parallelism(c),
-                   "timing": "sum of per-tile kernel times (HIP events) + all-gather times; inputs "
-                             "regenerated per tile outside the timed region (1.02 TB > 288 GB HBM)"},
-        "roofline": roofline(4 * T * (K + 2), k_ms / per, traffic_for("cfg3", T, K)),
+                               f"({peer_bytes/1e12:.3f} TB); {per} tile(s) of {T:,} coords per GPU, "
+                               f"{chunks} chunks per tile", "tiles_per_gpu": per, "parallelism": parallelism(c),
+                   "timing": "sum over tiles of first-kernel-start -> last-all-gather-end (HIP events; "
+                             "all-gather of chunk s overlapped with chunk s+1); inputs regenerated per tile "
+                             "outside the timed region (1.02 TB > 288 GB HBM)"},
+        "roofline": roofline(4 * C * (K + 2), k_ms / (per * chunks), traffic_for("cfg3-chunk", C, K)),
     }
 
 

@@ -14,8 +14,10 @@
 // checked) by gen_networks.py into networks.inc.
 //
 // K <= 128: ONE LANE per coordinate (KP = next power of two, +inf pads; a
-// network pruned to the wanted ranks when K == KP in {64, 128}, run on the
-// float values when the wave holds no NaN -- robust_nets.h).  Loads:
+// network pruned to the wanted ranks when K == KP in {64, 128}).  The float
+// network of robust_nets.h is NOT used here: holding the float copy next to
+// the keys took the K = 128 kernels from 146 / 183 VGPRs (3 / 2 waves per
+// SIMD) to 256 (1 wave) and cfg4 from 73% / 60% to 59% / 52% of HBM peak.  Loads:
 // each wave instruction reads 256 contiguous bytes of one peer; all KP loads
 // are issued before the first compare.  K in 129..256 is robust_lds.hip.
 #include "robust_nets.h"
@@ -38,23 +40,6 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
     v[j] = __float_as_uint(ldg_nt(p + i));
   }
   __builtin_amdgcn_sched_barrier(0);  // all KP loads in flight before the first use
-  if constexpr (MODE != 0) {  // K == KP: the float network when the wave holds no NaN
-    if (!wave_has_nan(v)) {
-      fk f[KP];
-#pragma unroll
-      for (int j = 0; j < KP; ++j) f[j].x = __uint_as_float(v[j]);
-      run_special<KP, MODE>(f);
-      if constexpr (RULE == P2P_RULE_MEDIAN) {
-        return f[(KP - 1) / 2].x;
-      } else {
-        constexpr int b = (KP * 2) / 10;
-        float acc = 0.f;
-#pragma unroll
-        for (int j = b; j < KP - b; ++j) acc = __fadd_rn(acc, f[j].x);
-        return acc / static_cast<float>(KP - 2 * b);
-      }
-    }
-  }
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
     const bool real = (MODE != 0) || (j < K);

@@ -55,6 +55,10 @@ __device__ __forceinline__ u16x2 pmax(u16x2 a, u16x2 b) { return __builtin_eleme
 #ifndef P2P_LDS_DIAG
 #define P2P_LDS_DIAG 0
 #endif
+// A/B build only (make nofloat): the uint32-key network for every wave.
+#ifndef P2P_NO_FLOAT_PATH
+#define P2P_NO_FLOAT_PATH 0
+#endif
 
 namespace p2p {
 
@@ -609,7 +613,7 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
       own = q == 0;
     } else {
       bool fast = false;  // every slot real (K == KP) and no NaN in the wave: the float network
-      if constexpr (MODE != 0) fast = !wave_has_nan(v);
+      if constexpr (MODE != 0 && !P2P_NO_FLOAT_PATH) fast = !wave_has_nan(v);
       if (fast) {
         fk f[H];
 #pragma unroll
