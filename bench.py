@@ -162,6 +162,16 @@ def bits_equal(a, b) -> bool:
 
 
 # ------------------------------------------------------------------ flat rules
+PITCH = 64  # fp32 elements: every peer chunk starts a 256-B boundary
+
+
+def pitched_slab(K, S, C, dev):
+    """[K, S, C'] fp32 with C' = C rounded up to PITCH: peer p's chunk s is
+    slab[p, s, :C], 256-B aligned like a separate allocation (a 16-B aligned
+    chunk straddles one more 128-B HBM line per 4-KiB kernel tile)."""
+    return torch.empty((K, S, -(-C // PITCH) * PITCH), dtype=torch.float32, device=dev)
+
+
 def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chunks):
     """Resident [K, n] slab per rank; a step = the rule over it (+ the chunked
     all-gather at N > 1).  Returns (record, ms_per_step)."""
@@ -174,13 +184,13 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
     if need > free * 0.97:
         raise SystemExit(f"{name}: needs {need/1e9:.1f} GB, {free/1e9:.1f} GB free")
     log(f"[rank {rank}] {name}: generating {K} x {n:,} fp32 peer slab ({K*n*4/1e9:.1f} GB)")
-    slab = torch.empty((K, n), dtype=torch.float32, device=dev)
-    for p in range(K):
-        ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE, C, world, rank)
-    w = torch.empty(n, dtype=torch.float32, device=dev)
-    ops.fill_synthetic_(w, seed, W_PEER, W_SCALE, C, world, rank)
+    slab, w = pitched_slab(K, S, C, dev), pitched_slab(1, S, C, dev)[0]
+    for s in range(S):  # local chunk s is global chunk s*N + rank
+        for p in range(K):
+            ops.fill_synthetic_(slab[p, s, :C], seed, p, UPD_SCALE, C, world, rank + s * world)
+        ops.fill_synthetic_(w[s, :C], seed, W_PEER, W_SCALE, C, world, rank + s * world)
     w_full = torch.empty(n * world, dtype=torch.float32, device=dev) if world > 1 else None
-    tables = [ops.pointer_table([slab[p, s * C:(s + 1) * C] for p in range(K)], dev) for s in range(S)]
+    tables = [ops.pointer_table([slab[p, s, :C] for p in range(K)], dev) for s in range(S)]
     torch.cuda.synchronize()
     comp = torch.cuda.current_stream(dev)
     comm = torch.cuda.Stream(dev)
@@ -188,7 +198,7 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
 
     def step(record=False):
         for s in range(S):
-            ws = w[s * C:(s + 1) * C]
+            ws = w[s, :C]
             if record:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(comp)
@@ -215,7 +225,7 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
         if i == 0 and check:
             torch.cuda.synchronize()
             bad = [g for g in range(world)
-                   if not bits_equal((w_full[g * C:g * C + m] if world > 1 else w[:m]).cpu().numpy(),
+                   if not bits_equal((w_full[g * C:g * C + m] if world > 1 else w[0, :m]).cpu().numpy(),
                                      oracle_expect(rule, K, m, seed, C, world, g))]
             log(f"[rank 0] {name}: spot check vs oracle ({m} coords x {world} rank chunk(s)): "
                 f"{'bit-exact' if not bad else f'MISMATCH on ranks {bad}'}")
@@ -294,10 +304,9 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
     if nchunks % (world * chunks):
         raise SystemExit(f"cfg3-full: {nchunks} chunks do not split into tiles of {chunks} over {world} GPUs")
     per = nchunks // (world * chunks)  # tiles per rank
-    slab = torch.empty((K, T), dtype=torch.float32, device=dev)
-    w = torch.empty(T, dtype=torch.float32, device=dev)
+    slab, w = pitched_slab(K, chunks, C, dev), pitched_slab(1, chunks, C, dev)[0]
     w_full = torch.empty(CFG3_COORDS, dtype=torch.float32, device=dev) if world > 1 else None
-    tables = [ops.pointer_table([slab[p, s * C:(s + 1) * C] for p in range(K)], dev) for s in range(chunks)]
+    tables = [ops.pointer_table([slab[p, s, :C] for p in range(K)], dev) for s in range(chunks)]
     comp = torch.cuda.current_stream(dev)
     comm = torch.cuda.Stream(dev)
     wall, kern, gath = [], [], []
@@ -308,9 +317,10 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
             # local chunk s of tile u is global chunk (u*chunks + s)*N + rank: in the
             # synthetic generator that is "rank" r + u*chunks*N of an N-rank chunk map
             vr = rank + u * chunks * world
-            for p in range(K):
-                ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE, C, world, vr)
-            ops.fill_synthetic_(w, seed, W_PEER, W_SCALE, C, world, vr)
+            for s in range(chunks):
+                for p in range(K):
+                    ops.fill_synthetic_(slab[p, s, :C], seed, p, UPD_SCALE, C, world, vr + s * world)
+                ops.fill_synthetic_(w[s, :C], seed, W_PEER, W_SCALE, C, world, vr + s * world)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -320,14 +330,14 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
             for s in range(chunks):
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
                 e[0].record(comp)
-                ops.aggregate(None, "fedavg", w=w[s * C:(s + 1) * C], lr=0.1, table=tables[s])
+                ops.aggregate(None, "fedavg", w=w[s, :C], lr=0.1, table=tables[s])
                 e[1].record(comp)
                 if world > 1:
                     comm.wait_event(e[1])
                     g0 = ((u * chunks + s) * world) * C
                     with torch.cuda.stream(comm):
                         e[2].record(comm)
-                        dist.all_gather_into_tensor(w_full[g0:g0 + world * C], w[s * C:(s + 1) * C])
+                        dist.all_gather_into_tensor(w_full[g0:g0 + world * C], w[s, :C])
                         e[3].record(comm)
                 ev.append(e)
             comp.wait_stream(comm)
@@ -340,7 +350,7 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
                 g_tot += sum(e[2].elapsed_time(e[3]) for e in ev)
             if not checked and not args.no_check and rank == 0:
                 m = 4096
-                got = (w_full[:m] if world > 1 else w[:m]).cpu().numpy()  # global chunk 0: rank 0, tile 0
+                got = (w_full[:m] if world > 1 else w[0, :m]).cpu().numpy()  # global chunk 0: rank 0, tile 0
                 ok = bits_equal(got, oracle_expect("fedavg", K, m, seed, C, world, 0))
                 log(f"[rank 0] cfg3-full: spot check of global chunk 0 vs oracle: {'bit-exact' if ok else 'MISMATCH'}")
                 if not ok:
@@ -424,18 +434,18 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
         for i, p in enumerate(model.parameters()):
             p.view(-1).copy_(flat_w[offs[i]:offs[i + 1]])
     # the updates live where DeviceInbox lands received updates: rows of one
-    # [K, N] slab (every tensor size here is a multiple of 4, so the row
-    # layout is the plain concatenation), generated on device
+    # [K, N'] slab (tensors at 256-B aligned offsets), generated on device
     from p2pdl_amd.node.inbox import DeviceInbox
 
     inbox = DeviceInbox(model.state_dict(), k_max=K, device=dev)
-    assert inbox.row == n
     slab = inbox.slab
     for p in range(K):
         ops.fill_synthetic_(slab[p], seed, p, UPD_SCALE)
     landed = [inbox.view(j) for j in range(K)]
     keys = [nm.replace(".", "__") for nm, _ in shapes]
-    plain = [{k: slab[j, offs[i]:offs[i + 1]].view(shapes[i][1]) for i, k in enumerate(keys)} for j in range(K)]
+    assert inbox.layout[keys[0]][0] == 0 and sizes[0] >= 4096  # the spot check's coordinates
+    plain = [{k: slab[j, inbox.layout[k][0]:inbox.layout[k][0] + sizes[i]].view(shapes[i][1])
+              for i, k in enumerate(keys)} for j in range(K)]
     updates = landed
     node = types.SimpleNamespace(model=model, trainers_list=[0] * K, addr="127.0.0.1", port=1, neighbors=[],
                                  received_models=[])
@@ -491,8 +501,8 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
     finally:
         agg.broadcast_global_model_update = saved
     call_ms = sum(a.elapsed_time(b) for a, b in ev_fast) / len(ev_fast)
-    # the same bytes through the flat C-ABI kernel (one buffer per peer), for comparison
-    table = ops.pointer_table(list(slab), dev)
+    # the same byte count through the flat C-ABI kernel (one buffer per peer), for comparison
+    table = ops.pointer_table([slab[p, :n] for p in range(K)], dev)
     fe = []
     for i in range(steps + 2):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

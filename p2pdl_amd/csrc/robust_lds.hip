@@ -180,6 +180,19 @@ __device__ __forceinline__ float reduce_keys(T (&v)[H], int q, int K, int trim_b
     sort_full<H>(v);
 #pragma unroll
     for (int s = 2; s <= L; s *= 2) {
+      if constexpr (RULE == P2P_RULE_MEDIAN && MODE == 1) {
+        if (s == L) {  // last flip: slices q < L/2 keep the K/2 smallest; the median is their max.
+          // Only those lanes' results are used, so each pair is ONE v_min with
+          // the partner's register as a DPP operand (no v_mov_dpp, no med3),
+          // reduced by v_max3.
+          T mx = min(v[0], L == 2 ? xq<1>(v[H - 1]) : xq<3>(v[H - 1]));
+#pragma unroll
+          for (int j = 1; j < H; ++j) mx = max(mx, min(v[j], L == 2 ? xq<1>(v[H - 1 - j]) : xq<3>(v[H - 1 - j])));
+          if constexpr (L == 4) mx = max(mx, xq<1>(mx));
+          own = (q == 0);
+          return value(mx);
+        }
+      }
       {  // flip against the mirrored lane of the s-lane group
         const T lim = keep_limit(v[0], (q & (s / 2)) != 0);
 #pragma unroll
@@ -189,16 +202,6 @@ __device__ __forceinline__ float reduce_keys(T (&v)[H], int q, int K, int trim_b
           const T pb = (s == 2) ? xq<1>(a) : xq<3>(a);  // partner's v[j]
           v[j] = keep(a, pa, lim);
           v[H - 1 - j] = keep(b, pb, lim);
-        }
-      }
-      if constexpr (RULE == P2P_RULE_MEDIAN && MODE == 1) {
-        if (s == L) {  // slices q < L/2 now hold the K/2 smallest keys; median = their max
-          T mx = v[0];
-#pragma unroll
-          for (int j = 1; j < H; ++j) mx = max(mx, v[j]);
-          if constexpr (L == 4) mx = max(mx, xq<1>(mx));
-          own = (q == 0);
-          return value(mx);
         }
       }
 #pragma unroll
@@ -426,20 +429,23 @@ __device__ __forceinline__ void block_sync_lds() {
 // next tile in flight while the sorters work on the current one.  Per tile:
 //   loaders: wait own pieces of tile t | barrier A | barrier B | DMA(t+2 grid)
 //   sorters: (fill if not DMA-able)   | barrier A | read      | barrier B | sort, store
-template <int L, int H, int RULE, int MODE, bool SEGS, int NB, int PK = 1>
-__global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __restrict__ peers,
+template <int L, int H, int RULE, int MODE, bool SEGS, int NB, int PK = 1, bool SELF = false>
+__global__ __launch_bounds__(SELF ? 256 : 512) __attribute__((amdgpu_waves_per_eu(SELF ? 2 : 1)))
+void robust_lds_kernel(const float* const* __restrict__ peers,
                                                              const Seg* __restrict__ segs, int nseg,
                                                              int64_t ntiles, int K, int trim_b, int64_t n,
                                                              float* w, float* out, float lr) {
   using Lay = LdsLayout<L, H, NB, PK>;
-  static_assert(128 * Lay::W == 512, "launch bounds");
+  static_assert((SELF ? 64 : 128) * Lay::W == (SELF ? 256 : 512), "launch bounds");
+  static_assert(!SELF || (Lay::NBUF == 1 && PK == 1), "self-staged: one image, two blocks per CU");
   static_assert(PK == 1 || (L == 4 && H == 64 && RULE == P2P_RULE_MEDIAN && MODE == 1), "radix16: median of 256");
   __shared__ __attribute__((aligned(16))) uint8_t lds_raw[Lay::BYTES];
   uint8_t P2P_LDS* lds = (uint8_t P2P_LDS*)lds_raw;
   const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
-  const bool loader = wi >= Lay::W;  // wave-uniform role
-  const int li = wi - Lay::W;        // loader index
+  const bool loader = !SELF && wi >= Lay::W;  // wave-uniform role
+  const bool issuer = SELF || loader;          // issues the LDS-DMA
+  const int li = SELF ? wi : wi - Lay::W;      // DMA share index
   const int q = lane % L, c = wi * Lay::TW + lane / L;  // sorters: coordinate inside the block tile
 
   const int64_t nb = gridDim.x;
@@ -507,14 +513,14 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
   TileSrc cur = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t);
   bind(cur);
   bool dma_cur = dma_ok(cur);
-  if (loader && dma_cur) issue(cur, 0);
+  if (issuer && dma_cur) issue(cur, 0);
   TileSrc nx1 = cur;
   bool dma_nx1 = false;
   if (D == 2 && t + nb < ntiles) {
     nx1 = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, t + nb);
     bind(nx1);
     dma_nx1 = dma_ok(nx1);
-    if (loader && dma_nx1) issue(nx1, Lay::IMG);
+    if (issuer && dma_nx1) issue(nx1, Lay::IMG);
   }
   int img = 0;
   // the tile D grids ahead of t: located, and DMA'd by the loaders
@@ -525,7 +531,7 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
       nxd = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, tt + D * nb);
       bind(nxd);
       dma_nxd = dma_ok(nxd);
-      if (loader && dma_nxd) issue(nxd, img);
+      if (issuer && dma_nxd) issue(nxd, img);
     }
     if constexpr (D == 2) {
       cur = nx1;
@@ -556,6 +562,7 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
       fill_direct<L, H, PK>(im, me.peers, me.w, me.n, i, K, q, c);
       if constexpr (PK == 2) fill_direct<L, H, PK>(im, me.peers, me.w, me.n, i + 64 / L, K, q, c + 64 / L);
     }
+    if constexpr (SELF) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // own pieces landed
     __builtin_amdgcn_s_barrier();  // A: every piece of tile t is in the image
     asm volatile("" ::: "memory");
     uint32_t v[H];
@@ -648,39 +655,40 @@ struct LdsArgs {
   hipStream_t stream;
 };
 
-template <int L, int H, int RULE, int MODE, bool SEGS, int NB, int PK = 1>
+template <int L, int H, int RULE, int MODE, bool SEGS, int NB, int PK = 1, bool SELF = false>
 static void launch_lds_kernel(const LdsArgs& a) {
   using Lay = LdsLayout<L, H, NB, PK>;
-  auto kern = robust_lds_kernel<L, H, RULE, MODE, SEGS, NB, PK>;
+  auto kern = robust_lds_kernel<L, H, RULE, MODE, SEGS, NB, PK, SELF>;
+  constexpr int kThreads = (SELF ? 64 : 128) * Lay::W;
   static int resident = 0;  // persistent grid: every resident block slot once
   if (resident == 0) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 128 * Lay::W, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), kThreads, 0);
     resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
   }
   const int64_t ntiles = SEGS ? a.tiles : ceil_div(a.n, Lay::TB);
   const int64_t grid = ntiles < resident ? ntiles : resident;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(128 * Lay::W), 0, a.stream, a.peers, a.segs, a.nseg,
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, a.stream, a.peers, a.segs, a.nseg,
                      ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
 }
 
-template <int L, int H, int RULE, int MODE, int NB>
+template <int L, int H, int RULE, int MODE, int NB, bool SELF>
 static void launch_lds_mode(const LdsArgs& a) {
-  if (a.segs) launch_lds_kernel<L, H, RULE, MODE, true, NB>(a);
-  else launch_lds_kernel<L, H, RULE, MODE, false, NB>(a);
+  if (a.segs) launch_lds_kernel<L, H, RULE, MODE, true, NB, 1, SELF>(a);
+  else launch_lds_kernel<L, H, RULE, MODE, false, NB, 1, SELF>(a);
 }
 
-template <int L, int H, int RULE, int NB = 0>
+template <int L, int H, int RULE, int NB = 0, bool SELF = false>
 static void launch_lds(const LdsArgs& a) {
   constexpr int KP = L * H;
   if constexpr (RULE == P2P_RULE_MEDIAN) {
-    if (a.K == KP) return launch_lds_mode<L, H, RULE, 1, NB>(a);
+    if (a.K == KP) return launch_lds_mode<L, H, RULE, 1, NB, SELF>(a);
   } else {
-    if (a.K == KP && a.trim_b == (KP * 2) / 10) return launch_lds_mode<L, H, RULE, 2, NB>(a);
+    if (a.K == KP && a.trim_b == (KP * 2) / 10) return launch_lds_mode<L, H, RULE, 2, NB, SELF>(a);
   }
-  launch_lds_mode<L, H, RULE, 0, NB>(a);
+  launch_lds_mode<L, H, RULE, 0, NB, SELF>(a);
 }
 
 }  // namespace p2p

@@ -501,6 +501,9 @@ class LandedUpdate(OrderedDict):
         return (OrderedDict, ([(k, v.clone()) for k, v in self.items()],))
 
 
+ROW_ALIGN = 64  # fp32 elements (256 B) per tensor offset in a slab row
+
+
 class DeviceInbox:
     """[K_max, N] fp32 slab on the GPU for the updates of one round.
 
@@ -517,9 +520,11 @@ class DeviceInbox:
         off = 0
         for key, t in template.items():
             if t.dtype == torch.float32:
-                # 16-B aligned offsets so every row and every tensor view is DMA-friendly
+                # 256-B aligned offsets (and row pitch): every tensor view starts
+                # a 128-B HBM line, as a separate allocation would -- a 16-B
+                # aligned view straddles one more line per kernel tile
                 self.layout[key] = (off, tuple(t.shape), t.numel())
-                off += -(-t.numel() // 4) * 4
+                off += -(-t.numel() // ROW_ALIGN) * ROW_ALIGN
         self.row = off
         self.k_max = int(k_max)
         self.slab = torch.empty((self.k_max, self.row), dtype=torch.float32, device=self.device)
