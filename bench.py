@@ -709,6 +709,7 @@ def run_inbox_workload(args, K, n, seed, dev):
     a GPU sender (pickle of CUDA tensors, node/node.py:285) deserialized into
     device tensors -- the reference's pickle.loads vs DeviceInbox.land.
     value = update bytes landed per second (host-to-device, PCIe-bound)."""
+    import hashlib
     import pickle
 
     from p2pdl_amd.node.inbox import DeviceInbox
@@ -753,7 +754,32 @@ def run_inbox_workload(args, K, n, seed, dev):
         for s in ser:
             pickle.loads(s)
 
+    # + the tester's per-update digest (its echo signs the serialized update,
+    # node/node.py:144 -> utils/crypto.py:54-57): overlapped in land() vs after it
+    def ours_digest():
+        inbox.reset()
+        for s in ser:
+            inbox.land(s, digest=True)
+        return [inbox.digest(k) for k in range(len(ser))]
+
+    def land_then_hash():
+        inbox.reset()
+        for s in ser:
+            inbox.land(s)
+            hashlib.sha256(s).digest()
+
+    def reference_echo():
+        for s in ser:
+            pickle.loads(s)
+            hashlib.sha256(s).digest()
+
+    if not args.no_check:
+        ok = ours_digest() == [hashlib.sha256(s).digest() for s in ser]
+        log(f"overlapped digests == hashlib: {ok}")
+        if not ok:
+            raise SystemExit("bench: inbox digest differs from hashlib")
     t_ours, t_ref = timed(ours), timed(reference)
+    t_dig, t_seq, t_ref_dig = timed(ours_digest), timed(land_then_hash), timed(reference_echo)
     n = sum(_numel(s) for _, s in shapes)
     nbytes = K * n * 4
     print(json.dumps({
@@ -763,6 +789,11 @@ def run_inbox_workload(args, K, n, seed, dev):
         "config": {"workload": f"inbox: land {K} serialized updates of {n:,} params ({len(shapes)} tensors) "
                                f"in the device slab (SURVEY §8(f) row 1)", "reference_pickle_loads_gbs":
                    round(nbytes / t_ref / 1e9, 3), "reference_ms": round(t_ref * 1e3, 3),
+                   "with_digest": {"land_digest_overlapped_ms": round(t_dig * 1e3, 3),
+                                   "land_then_hashlib_ms": round(t_seq * 1e3, 3),
+                                   "reference_pickle_loads_then_hashlib_ms": round(t_ref_dig * 1e3, 3),
+                                   "what": "SHA-256 of each serialized update (the bytes the tester's echo "
+                                           "signs) on a hashing thread beside parse + copy + DMA"},
                    "parallelism": "single GPU, host-to-device"},
         "roofline": {"bound": "pcie (host-to-device)", "achieved": round(nbytes / t_ours / 1e9, 2), "peak": 63.0,
                      "unit": "GB/s", "frac": round(nbytes / t_ours / 1e9 / 63.0, 4), "traffic": None},

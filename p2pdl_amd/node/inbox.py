@@ -33,6 +33,7 @@ this on torch-produced pickles of the reference's message shapes).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import pickle
 import struct
@@ -530,6 +531,7 @@ class DeviceInbox:
         self.slab = torch.empty((self.k_max, self.row), dtype=torch.float32, device=self.device)
         self._stage = [torch.empty(self.row, dtype=torch.float32, pin_memory=True) for _ in range(2)]
         self._events = [None, None]
+        self._digests = {}
         self.count = 0
         # land() is called from the listener threads (one per connection,
         # reference node/node.py:89): row reservation and the staging ->
@@ -539,13 +541,23 @@ class DeviceInbox:
     def reset(self) -> None:
         with self._lock:
             self.count = 0
+            self._digests = {}
 
-    def land(self, serialized, k: int | None = None) -> dict:
+    def land(self, serialized, k: int | None = None, digest: bool = False) -> dict:
         """Parse one serialized update and copy it to slab row k (next free row
         by default).  Returns {key: tensor} in the update's key order, fp32
         entries as views of the slab row -- bit-identical to pickle.loads.
         The payloads go message buffer -> pinned staging row (one memcpy,
-        split across a thread pool) -> device (one DMA)."""
+        split across a thread pool) -> device (one DMA).
+
+        digest=True also starts SHA-256 of the serialized bytes -- what the
+        tester signs in its echo (node/node.py:144 -> utils/crypto.py:54-57)
+        -- on a hashing thread, overlapped with the parse, the staging copy
+        and the DMA of this update and the next; ``digest(k)`` returns it.
+        The buffer must not change until then.  (Host SHA-NI: one message is
+        one serial chain, ~1.4 GB/s on a host core vs ~35 MB/s on one GPU
+        lane -- DESIGN.md §3 K3.)"""
+        fut = _hash_pool().submit(_sha256, serialized) if digest else None
         raw = ZeroCopyParser(serialized).parse()
         with self._lock:
             if k is None:
@@ -553,7 +565,18 @@ class DeviceInbox:
             if not 0 <= k < self.k_max:
                 raise IndexError(f"slab row {k} out of range (k_max={self.k_max})")
             self.count = max(self.count, k + 1)
+            if fut is not None:
+                self._digests[k] = fut
             return self._land_locked(raw, k)
+
+    def digest(self, k: int) -> bytes:
+        """SHA-256 of the bytes landed in row k with ``land(..., digest=True)``
+        (waits for the hashing thread)."""
+        with self._lock:
+            fut = self._digests.get(k)
+        if fut is None:
+            raise KeyError(f"slab row {k} was not landed with digest=True")
+        return fut.result()
 
     def _land_locked(self, raw, k: int) -> dict:
         s = k & 1
@@ -598,6 +621,22 @@ class DeviceInbox:
 
 
 _POOL = None
+_HASH_POOL = None
+_POOL_LOCK = threading.Lock()
+
+
+def _sha256(buf) -> bytes:
+    return hashlib.sha256(buf).digest()  # releases the GIL for large buffers
+
+
+def _hash_pool():
+    global _HASH_POOL
+    with _POOL_LOCK:
+        if _HASH_POOL is None:
+            from concurrent.futures import ThreadPoolExecutor
+            _HASH_POOL = ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1),
+                                            thread_name_prefix="p2p-sha256")
+        return _HASH_POOL
 
 
 def _copy_all(jobs) -> None:
@@ -607,9 +646,10 @@ def _copy_all(jobs) -> None:
     big = [j for j in jobs if j[0].size >= (1 << 18)]
     small = [j for j in jobs if j[0].size < (1 << 18)]
     if big:
-        if _POOL is None:
-            from concurrent.futures import ThreadPoolExecutor
-            _POOL = ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1))
+        with _POOL_LOCK:  # land() runs on several listener threads
+            if _POOL is None:
+                from concurrent.futures import ThreadPoolExecutor
+                _POOL = ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1))
         pieces = []
         for dst, rt in big:  # split the large tensors into ~1M-element pieces
             src = rt.array().reshape(-1)

@@ -369,6 +369,43 @@ def test_device_inbox_concurrent_landing(cuda):
 
 
 @pytest.mark.gpu
+def test_device_inbox_digest_overlapped_with_landing(cuda):
+    """land(..., digest=True) hashes the serialized update --
+    the bytes the tester signs in its echo (node/node.py:144, crypto.py:54-57)
+    -- beside the parse / copy / DMA; digests equal hashlib's, concurrent
+    landings keep row <-> digest pairs, rows without digest refuse."""
+    import hashlib
+
+    k = 6
+    template = {name: torch.zeros(s, device=cuda) for name, s in MLP_SHAPES}
+    inbox = DeviceInbox(template, k_max=k + 1, device=cuda)
+    for key, (off, _, _) in inbox.layout.items():
+        assert off % 64 == 0, key  # 256-B aligned tensor views
+    ser = [pickle.dumps(mlp_update(70 + j)) for j in range(k)]
+    got = [None] * k
+    barrier = threading.Barrier(k)
+
+    def worker(j):
+        barrier.wait()
+        got[j] = inbox.land(ser[j], j, digest=True)
+
+    ths = [threading.Thread(target=worker, args=(j,)) for j in range(k)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(60)
+    for j in range(k):
+        assert inbox.digest(j) == hashlib.sha256(ser[j]).digest(), j
+        assert got[j].row == j
+    inbox.land(ser[0], k)
+    with pytest.raises(KeyError):
+        inbox.digest(k)
+    inbox.reset()
+    with pytest.raises(KeyError):
+        inbox.digest(0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rule", ["fedavg", "median", "trimmed"])
 def test_landed_updates_take_the_slab_fast_path(cuda, rule, monkeypatch):
     """aggregate_models on DeviceInbox-landed updates builds its kernel table
