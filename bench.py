@@ -853,6 +853,9 @@ def main():
         sub = {}
         if not args.no_sub and args.workload == "cfg3" and not (args.coords or args.peers):
             sub["cfg3_full"] = measure_cfg3_full(c, args)
+            if main_rec.get("cpu_baseline"):  # the same rule and op sequence as the main line
+                sub["cfg3_full"]["cpu_baseline"] = dict(main_rec["cpu_baseline"], note="the cfg3 line's CPU run "
+                                                        "(same rule, per-coordinate cost independent of N)")
             if world == 1:
                 for name in SUB_N1:
                     r, k2, n2, s2 = WORKLOADS[name]
