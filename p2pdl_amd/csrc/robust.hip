@@ -47,6 +47,13 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
   }
   if constexpr (MODE == 0) {
     sort_full<KP>(v);
+  } else if constexpr (RULE == P2P_RULE_TRIMMED && KP == 128) {  // fewer live VGPRs: 3 waves/SIMD
+    kx x[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) x[j].k = v[j];
+    run_special<KP, MODE>(x);
+#pragma unroll
+    for (int j = 0; j < KP; ++j) v[j] = x[j].k;
   } else {
     run_special<KP, MODE>(v);
   }
