@@ -25,14 +25,16 @@ namespace p2p {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-// One float4 per lane per peer per tile (1024 floats, 56 VGPRs, full
-// occupancy) for flat buffers AND state_dict segments.  Measured against
-// 4096-float tiles: cfg2 (64 x 11.7M) 76.8% vs 71.4% of HBM peak -- 2854
-// tiles of 4096 leave the last wave of blocks part-empty, and the 4-float4
-// segment kernel needed 150 VGPRs (occupancy 3) -- and cfg3 (256 x 125M)
-// 77.9% vs 77.1%.
-constexpr int kNV = 1;
-constexpr int kTile = kBlock * 4 * kNV;   // 1024 floats per tile
+// Four float4 per lane per peer per tile (4096 floats) for flat buffers AND
+// state_dict segments: 4 x 8 independent 1-KiB wave loads in flight per lane.
+// Only the full-tile path is 4-wide; the ragged last tile of a buffer runs as
+// four 1024-float sub-tiles, so the kernels stay at 64 / 74 VGPRs (round 1's
+// 4-wide ragged path took the segment kernel to 150 VGPRs and lost to one
+// float4 per lane).  Round 2 A/B against one float4 per lane, same box
+// (profiles/r02/ab/abfa4): cfg3 21.02 vs 21.25 ms, cfg2 0.518 vs 0.522 ms;
+// the standalone sweep (tools/fedavg_sweep.hip) shows the same order.
+constexpr int kNV = 4;
+constexpr int kTile = kBlock * 4 * kNV;   // 4096 floats per tile
 template <int NV> constexpr int tile_of() { return kBlock * 4 * NV; }
 constexpr int kUnroll = 8;
 
@@ -120,12 +122,13 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
       fedavg_tile_vec<NV, true>(peers, K, n, base, w, out, lr);
       return;
     }
-    fedavg_tile_vec<NV, false>(peers, K, n, base, w, out, lr);
-    // trailing elements of a float4 group that straddles n
+    // ragged last tile: 1024-float sub-tiles (same per-element op order)
 #pragma unroll 1
     for (int v = 0; v < NV; ++v) {
       const int64_t g = base + kBlock * 4 * v;
-      if (g < n && g + 4 > n)
+      if (tile0 + kBlock * 4 * v >= n) break;
+      fedavg_tile_vec<1, false>(peers, K, n, g, w, out, lr);
+      if (g < n && g + 4 > n)  // trailing elements of a float4 group that straddles n
         for (int64_t i = g; i < n; ++i) fedavg_elem(peers, K, i, w, out, lr);
     }
     return;

@@ -119,7 +119,7 @@ def test_flat_fedavg_matches_reference_golden(cuda, case):
 
 
 @pytest.mark.parametrize("k", [1, 2, 3, 7, 8, 9, 16, 17, 64, 255])
-@pytest.mark.parametrize("n", [1, 7, 2048, 2049, 100_003])
+@pytest.mark.parametrize("n", [1, 7, 2048, 2049, 4096, 8191, 100_003])
 def test_fedavg_vs_oracle(cuda, k, n):
     seed = 1000 * k + n
     peers = [oracle.synth(n, seed, p, 1e-2) for p in range(k)]

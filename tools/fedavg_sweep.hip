@@ -157,15 +157,28 @@ int main(int argc, char** argv) {
   const int K = argc > 1 ? atoi(argv[1]) : 256;
   const long n = argc > 2 ? atol(argv[2]) : 32L * 1024 * 1024;
   const int rounds = argc > 3 ? atoi(argv[3]) : 3;
+  // argv[4]: peer row pitch in floats (default n; -1 = one hipMalloc per peer);
+  // argv[5]: 1 = only the product-like variants
+  const long pitch = argc > 4 ? atol(argv[4]) : n;
+  const bool few = argc > 5 && atoi(argv[5]) == 1;
   float* slab; float* w; float* tmp; float* sink;
-  CHECK(hipMalloc(&slab, sizeof(float) * (size_t)K * n));
+  std::vector<const float*> hp(K);
+  if (pitch > 0) {
+    CHECK(hipMalloc(&slab, sizeof(float) * (size_t)K * pitch));
+    hipLaunchKernelGGL(init, dim3(8192), dim3(256), 0, 0, slab, (long)K * pitch);
+    for (int k = 0; k < K; ++k) hp[k] = slab + (long)k * pitch;
+  } else {
+    for (int k = 0; k < K; ++k) {
+      float* r; CHECK(hipMalloc(&r, sizeof(float) * (size_t)n));
+      hipLaunchKernelGGL(init, dim3(8192), dim3(256), 0, 0, r, n);
+      hp[k] = r;
+    }
+    slab = const_cast<float*>(hp[0]);
+  }
   CHECK(hipMalloc(&w, sizeof(float) * n));
   CHECK(hipMalloc(&tmp, sizeof(float) * n * 4));
   CHECK(hipMalloc(&sink, 64));
-  hipLaunchKernelGGL(init, dim3(8192), dim3(256), 0, 0, slab, (long)K * n);
   hipLaunchKernelGGL(init, dim3(8192), dim3(256), 0, 0, w, n);
-  std::vector<const float*> hp(K);
-  for (int k = 0; k < K; ++k) hp[k] = slab + (long)k * n;
   const float** dp; CHECK(hipMalloc(&dp, sizeof(void*) * K));
   CHECK(hipMemcpy(dp, hp.data(), sizeof(void*) * K, hipMemcpyHostToDevice));
   CHECK(hipDeviceSynchronize());
@@ -196,6 +209,8 @@ int main(int argc, char** argv) {
     VI("i4u4nt g4096 chk", 4, 4, true, true, 4096),
     VI("i1u16nt onetile chk", 1, 16, true, true, 0),
   };
+  if (few) vars = {VI("i1u8nt onetile chk", 1, 8, true, true, 0), VI("i4u8nt onetile", 4, 8, true, false, 0)};
+  printf("pitch %ld floats (%s)\n", pitch, pitch > 0 ? "one slab" : "one allocation per peer");
 
   std::vector<std::vector<float>> ms(vars.size());
   hipEvent_t e0, e1; CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
@@ -218,7 +233,7 @@ int main(int argc, char** argv) {
   }
   // roofs over the slab (K*n floats)
   const long n4 = (long)K * n / 4;
-  for (int r = 0; r < 2; ++r) {
+  for (int r = 0; r < (pitch > 0 && !few ? 2 : 0); ++r) {
     CHECK(hipEventRecord(e0, 0));
     hipLaunchKernelGGL(read_roof, dim3(8192), dim3(256), 0, 0, (const f4*)slab, n4, sink);
     CHECK(hipEventRecord(e1, 0)); CHECK(hipEventSynchronize(e1));
