@@ -458,7 +458,7 @@ void robust_lds_kernel(const float* const* __restrict__ peers,
   // on a pointer load while the next tile's DMA is outstanding); with one
   // image they are reloaded per tile (L2 hits) so the sorters' 128 keys keep
   // the register file.
-  constexpr bool kCachePtr = Lay::NBUF == 2 || PK == 2;  // radix16: one image, VGPRs to spare
+  constexpr bool kCachePtr = Lay::NBUF == 2 || PK == 2 || SELF;  // radix16 / self-staged: VGPRs to spare
   const float* rp[kCachePtr ? Lay::NCHW : 1];
   int64_t cur_seg = -1;
   bool aligned = false;
@@ -472,7 +472,7 @@ void robust_lds_kernel(const float* const* __restrict__ peers,
     cur_seg = s.seg;
     aligned = all_aligned16(s.peers, K, s.w, nullptr);
     if constexpr (kCachePtr) {
-      if (loader) {
+      if (issuer) {
 #pragma unroll
         for (int m = 0; m < Lay::NCHW; ++m) rp[m] = table_at(s.peers, row_of(m));
       }
@@ -642,6 +642,127 @@ void robust_lds_kernel(const float* const* __restrict__ peers,
   }
 }
 
+// Two sorter groups per block (lab variant 7): 2 x 4 sorter waves + 4 loader
+// waves = 12 waves, 3 per SIMD, so every SIMD has TWO sorting waves to issue
+// from (a lone sorter wave leaves ~11% of its cycles idle on LDS latency and
+// barriers).  Group g sorts the tiles of image g: iteration i covers tiles
+// t + 2i*grid (image 0) and t + (2i+1)*grid (image 1); the loaders refill both
+// images as soon as both groups have read them (one DMA period of slack, not
+// two).  768-lane blocks cap the kernel at 168 VGPRs: uint32-key network only.
+template <int RULE, int MODE, bool SEGS>
+__global__ __launch_bounds__(768) void robust_lds_g2_kernel(const float* const* __restrict__ peers,
+                                                            const Seg* __restrict__ segs, int nseg,
+                                                            int64_t ntiles, int K, int trim_b, int64_t n,
+                                                            float* w, float* out, float lr) {
+  constexpr int L = 4, H = 64;
+  using Lay = LdsLayout<L, H>;
+  static_assert(Lay::NBUF == 2 && Lay::W == 4, "one image per sorter group");
+  __shared__ __attribute__((aligned(16))) uint8_t lds_raw[Lay::BYTES];
+  uint8_t P2P_LDS* lds = (uint8_t P2P_LDS*)lds_raw;
+  const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const bool loader = wi >= 2 * Lay::W;  // wave-uniform role
+  const int g = loader ? 0 : wi / Lay::W;
+  const int li = wi - 2 * Lay::W;
+  const int q = lane % L, c = (wi % Lay::W) * Lay::TW + lane / L;
+
+  const int64_t nb = gridDim.x;
+  int64_t t0 = blockIdx.x;
+  if ((nb & 7) == 0) t0 = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);  // XCD-contiguous tiles
+  if (t0 >= ntiles) return;  // block-uniform
+  const int64_t iters = ceil_div(ceil_div(ntiles - t0, nb), 2);
+  auto tile_at = [&](int64_t i, int gg) { return t0 + (2 * i + gg) * nb; };
+
+  const float* rp[Lay::NCHW];
+  int64_t cur_seg = -1;
+  bool aligned = false;
+  auto row_of = [&](int m) {
+    const int ch = li * Lay::NCHW + m;
+    const int row = (ch / Lay::CPS) * H + (ch % Lay::CPS) * Lay::RPP + lane / Lay::LPR;
+    return row < K ? row : K - 1;
+  };
+  auto bind = [&](const TileSrc& s) {
+    if (s.seg == cur_seg) return;
+    cur_seg = s.seg;
+    aligned = all_aligned16(s.peers, K, s.w, nullptr);
+    if (loader) {
+#pragma unroll
+      for (int m = 0; m < Lay::NCHW; ++m) rp[m] = table_at(s.peers, row_of(m));
+    }
+  };
+  auto dma_ok = [&](const TileSrc& s) { return aligned && s.c0 + Lay::TB <= s.n; };
+  auto real_piece = [&](int m) {
+    const int ch = li * Lay::NCHW + m;
+    return MODE != 0 || (ch / Lay::CPS) * H + (ch % Lay::CPS) * Lay::RPP < K;
+  };
+  auto issue = [&](const TileSrc& s, int img_off) {
+    uint8_t P2P_LDS* im = lds + img_off;
+    const int64_t off = s.c0 + 4 * (lane % Lay::LPR);
+#pragma unroll
+    for (int m = 0; m < Lay::NCHW; ++m) {
+      const int ch = li * Lay::NCHW + m;
+      if (real_piece(m)) glds16(rp[m] + off, im + (ch / Lay::CPS) * Lay::SB + (ch % Lay::CPS) * 1024);
+    }
+    if (s.w && li == 0 && lane < Lay::LPR) glds16(s.w + s.c0 + 4 * lane, im + Lay::WOFF);
+  };
+  auto stage = [&](int64_t i) {  // loaders: DMA of iteration i's tiles into images 0 and 1
+#pragma unroll
+    for (int gg = 0; gg < 2; ++gg) {
+      const int64_t tt = tile_at(i, gg);
+      if (tt < ntiles) {
+        const TileSrc s = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, tt);
+        bind(s);
+        if (dma_ok(s)) issue(s, gg * Lay::IMG);
+      }
+    }
+  };
+
+  if (loader) {
+    stage(0);
+    for (int64_t i = 0; i < iters; ++i) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this loader's pieces of iteration i landed
+      __builtin_amdgcn_s_barrier();                     // A
+      __builtin_amdgcn_s_barrier();                     // B: both groups have read their image
+      asm volatile("" ::: "memory");
+      stage(i + 1);
+    }
+    return;
+  }
+  uint8_t P2P_LDS* im = lds + g * Lay::IMG;
+  for (int64_t i = 0; i < iters; ++i) {
+    const int64_t tt = tile_at(i, g);
+    const bool has = tt < ntiles;  // the last iteration may hold one tile only
+    TileSrc me{};
+    if (has) {
+      me = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, tt);
+      bind(me);
+      if (!dma_ok(me)) fill_direct<L, H, 1>(im, me.peers, me.w, me.n, me.c0 + c, K, q, c);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // A: both images hold their tiles
+    asm volatile("" ::: "memory");
+    uint32_t v[H];
+    const uint32_t P2P_LDS* sl = (const uint32_t P2P_LDS*)(im + q * Lay::SB) + c;
+#pragma unroll
+    for (int j = 0; j < H; ++j) v[j] = sl[j * (Lay::RB / 4)];
+    const float wv = (has && me.w) ? ((const float P2P_LDS*)(im + Lay::WOFF))[c] : 0.f;
+    block_sync_lds();  // B: images consumed
+    if (!has) continue;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const bool real = (MODE != 0) || (q * H + j < K);
+      v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;
+    }
+    bool own = false;
+    const float agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
+    const int64_t e = me.c0 + c;
+    if (own && e < me.n) {
+      if (me.out) stg(me.out + e, agg);
+      if (me.w) stg(me.w + e, apply_lr(wv, lr, agg));
+    }
+  }
+}
+
 struct LdsArgs {
   const float* const* peers;
   const Seg* segs;
@@ -674,6 +795,37 @@ static void launch_lds_kernel(const LdsArgs& a) {
                      ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
 }
 
+template <int RULE, int MODE, bool SEGS>
+static void launch_lds_g2_kernel(const LdsArgs& a) {
+  using Lay = LdsLayout<4, 64>;
+  auto kern = robust_lds_g2_kernel<RULE, MODE, SEGS>;
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 768, 0);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  const int64_t ntiles = SEGS ? a.tiles : ceil_div(a.n, Lay::TB);
+  const int64_t grid = ntiles < resident ? ntiles : resident;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(768), 0, a.stream, a.peers, a.segs, a.nseg,
+                     ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
+}
+
+template <int RULE>
+static void launch_lds_g2(const LdsArgs& a) {
+  constexpr int KP = 256;
+  const bool special = RULE == P2P_RULE_MEDIAN ? a.K == KP : (a.K == KP && a.trim_b == (KP * 2) / 10);
+  if (special) {
+    if (a.segs) launch_lds_g2_kernel<RULE, RULE == P2P_RULE_MEDIAN ? 1 : 2, true>(a);
+    else launch_lds_g2_kernel<RULE, RULE == P2P_RULE_MEDIAN ? 1 : 2, false>(a);
+  } else {
+    if (a.segs) launch_lds_g2_kernel<RULE, 0, true>(a);
+    else launch_lds_g2_kernel<RULE, 0, false>(a);
+  }
+}
+
 template <int L, int H, int RULE, int MODE, int NB, bool SELF>
 static void launch_lds_mode(const LdsArgs& a) {
   if (a.segs) launch_lds_kernel<L, H, RULE, MODE, true, NB, 1, SELF>(a);
@@ -695,8 +847,9 @@ static void launch_lds(const LdsArgs& a) {
 
 using namespace p2p;
 
-// K in 129..256: 4 lanes x 64 keys per coordinate (p2p_robust_lds_tile and the
-// launch must agree; the tile size is a pure function of (rule, k)).  Other
+// K in 129..256: 4 lanes x 64 keys per coordinate, 64-coordinate tiles in
+// both block shapes (p2p_robust_lds_tile and the launch must agree; the tile
+// size is a pure function of (rule, k)).  Other
 // instantiations of the templates above (4 x 32, 2 x 64, 1 x 128, radix16)
 // are built only into the A/B library of tools/robust_lab.hip.
 extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t rule, int32_t k) {
@@ -705,11 +858,25 @@ extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t rule, int32_t k) {
   return LdsLayout<4, 64>::TB;
 }
 
+// K = 256 with the default trim (the pruned networks, float fast path): one
+// sorter group per block.  Any other K in 129..255 or trim runs the generic
+// padded network -- ~1.4x the instructions -- where two sorter groups per
+// block are faster (median -7%, trimmed -12% time for K in 129..255, round-2
+// lab A/B, profiles/r02/ab/labg2k); for the pruned K = 256 networks the
+// single-buffered images of the two-group block expose the DMA (median +27%).
 extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, const p2p_segment_t* segs,
                                                    int32_t nseg, int64_t tiles, int32_t k, int32_t rule,
                                                    int32_t trim_b, int64_t n, float* w, float* out, float lr,
                                                    p2p_stream_t stream) {
   LdsArgs a{peers, segs, nseg, tiles, k, trim_b, n, w, out, lr, static_cast<hipStream_t>(stream)};
-  if (rule == P2P_RULE_MEDIAN) launch_lds<4, 64, P2P_RULE_MEDIAN>(a);
-  else launch_lds<4, 64, P2P_RULE_TRIMMED>(a);
+  const bool med = rule == P2P_RULE_MEDIAN;
+  const bool pruned = k == 256 && (med || trim_b == (256 * 2) / 10);
+  if (pruned) {
+    if (med) launch_lds_mode<4, 64, P2P_RULE_MEDIAN, 1, 0, false>(a);
+    else launch_lds_mode<4, 64, P2P_RULE_TRIMMED, 2, 0, false>(a);
+  } else if (med) {
+    if (segs) launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, true>(a); else launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, false>(a);
+  } else {
+    if (segs) launch_lds_g2_kernel<P2P_RULE_TRIMMED, 0, true>(a); else launch_lds_g2_kernel<P2P_RULE_TRIMMED, 0, false>(a);
+  }
 }

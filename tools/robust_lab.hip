@@ -12,7 +12,8 @@ using namespace p2p;
 // variant: 0 product layout (4 lanes x 64 keys), 1 radix16 affine median
 // (K = 256 only), 2 LDS 4 x 32 (K <= 128), 3 LDS 2 x 64 (K <= 128),
 // 4 LDS 1 x 128 (K <= 128), 5 LDS 2 x 128 (K in 129..256), 6 self-staged 4 x 64
-// (no loader waves, one image, two blocks per CU; K in 129..256)
+// (no loader waves, one image, two blocks per CU; K in 129..256), 7 two sorter
+// groups per block (K in 129..256)
 extern "C" int32_t p2p_lab_robust(int32_t variant, const float* const* peers, int32_t k, int64_t n,
                                   int32_t rule, int32_t trim_b, float lr, float* w, float* out,
                                   p2p_stream_t stream) {
@@ -45,6 +46,10 @@ extern "C" int32_t p2p_lab_robust(int32_t variant, const float* const* peers, in
     case 6:  // self-staged: 4 waves sort AND issue the DMA, one image, two blocks per CU
       if (k <= 128) return P2P_ERR_UNSUPPORTED;
       if (med) launch_lds<4, 64, P2P_RULE_MEDIAN, 1, true>(a); else launch_lds<4, 64, P2P_RULE_TRIMMED, 1, true>(a);
+      break;
+    case 7:  // two sorter groups per block (12 waves: 2 x 4 sorters + 4 loaders), key network
+      if (k <= 128) return P2P_ERR_UNSUPPORTED;
+      if (med) launch_lds_g2<P2P_RULE_MEDIAN>(a); else launch_lds_g2<P2P_RULE_TRIMMED>(a);
       break;
     default:
       return P2P_ERR_INVALID;
