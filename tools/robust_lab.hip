@@ -51,6 +51,10 @@ extern "C" int32_t p2p_lab_robust(int32_t variant, const float* const* peers, in
       if (k <= 128) return P2P_ERR_UNSUPPORTED;
       if (med) launch_lds_g2<P2P_RULE_MEDIAN>(a); else launch_lds_g2<P2P_RULE_TRIMMED>(a);
       break;
+    case 8:  // two sorter groups per block, asynchronous (LDS counters instead of barriers)
+      if (k <= 128) return P2P_ERR_UNSUPPORTED;
+      if (med) launch_lds_g2a<P2P_RULE_MEDIAN>(a); else launch_lds_g2a<P2P_RULE_TRIMMED>(a);
+      break;
     default:
       return P2P_ERR_INVALID;
   }
