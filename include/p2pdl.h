@@ -60,7 +60,7 @@ const char *p2p_strerror(int32_t code);
 
 /* Elements per tile of the segment kernel for `rule` with k peers (host
  * planning helper for p2p_segment_t.tile_begin).  A pure function of
- * (rule, k): FedAvg 1024; median / trimmed 128 for k <= 128, 64 for
+ * (rule, k): FedAvg 4096; median / trimmed 128 for k <= 128, 64 for
  * k in 129..256. */
 int64_t p2p_tile_elems(int32_t rule, int32_t k);
 

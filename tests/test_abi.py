@@ -34,7 +34,7 @@ def test_abi_version_and_argument_errors_without_gpu():
     assert L.p2p_strerror(0) == b"ok"
     assert b"invalid" in L.p2p_strerror(-1)
     # tile sizes are a pure function of (rule, k): no process-wide layout state
-    assert L.p2p_tile_elems(0, 3) == 1024 and L.p2p_tile_elems(0, 256) == 1024
+    assert L.p2p_tile_elems(0, 3) == 4096 and L.p2p_tile_elems(0, 256) == 4096
     assert L.p2p_tile_elems(1, 64) == 128 and L.p2p_tile_elems(1, 128) == 128
     assert L.p2p_tile_elems(1, 129) == 64 and L.p2p_tile_elems(2, 200) == 64 and L.p2p_tile_elems(1, 256) == 64
     # argument validation happens before any HIP call
