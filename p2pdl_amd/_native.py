@@ -38,6 +38,7 @@ class P2PError(RuntimeError):
 
 _lib = None
 _lock = threading.Lock()
+_cuda_ok = False  # a ROCm device was seen (checked once)
 
 _P = ctypes.c_void_p
 _I32, _I64, _U64, _F32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
@@ -92,7 +93,10 @@ def require_device(t) -> None:
     """The hot path runs only on a ROCm device; CPU tensors are rejected."""
     import torch
 
-    if not torch.cuda.is_available():
+    global _cuda_ok
+    if not _cuda_ok:
+        _cuda_ok = torch.cuda.is_available()
+    if not _cuda_ok:
         raise NativeUnavailable("p2pdl_amd: no ROCm GPU visible; the HIP hot path cannot run "
                                 "(there is no CPU fallback)")
     if t.device.type != "cuda":

@@ -464,3 +464,54 @@ def test_landed_updates_take_the_slab_fast_path(cuda, rule, monkeypatch):
     back = pickle.loads(pickle.dumps(landed[0]))  # copies, not the slab
     assert type(back) is collections.OrderedDict and list(back) == list(landed[0])
     assert back["fc3.bias"].untyped_storage().nbytes() == 10 * 4
+
+
+@pytest.mark.gpu
+def test_slab_table_cache_across_rounds_and_streams(cuda, monkeypatch):
+    """The fast path caches its device segment table by the addresses and
+    sizes it encodes: round 2 reuses round 1's table for NEW values in the
+    same slab rows (bit-exact vs the oracle both rounds), a different row set
+    or model builds a new table, and a launch on another stream is correct."""
+    from p2pdl_amd import ops
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
+    k = 4
+    template = {name: torch.zeros(s, device=cuda) for name, s in MLP_SHAPES}
+    inbox = DeviceInbox(template, k_max=k + 1, device=cuda)
+    n = sum(int(np.prod(s)) for _, s in MLP_SHAPES)
+    w0 = oracle.synth(n, 9, 0xFFFFF, 5e-2)
+    model = torch.nn.Module()
+    offs = 0
+    for name, s in MLP_SHAPES:
+        m = int(np.prod(s))
+        mod, attr = name.split(".")
+        if not hasattr(model, mod):
+            model.add_module(mod, torch.nn.Module())
+        getattr(model, mod).register_parameter(attr, torch.nn.Parameter(
+            torch.from_numpy(w0[offs:offs + m].reshape(s).copy()).to(cuda)))
+        offs += m
+    node = types.SimpleNamespace(model=model, trainers_list=[0] * k, addr="a", port=1, neighbors=[],
+                                 received_models=[])
+    w = w0
+    for rnd, (rows, stream) in enumerate([(range(k), None), (range(k), None), (range(1, k + 1), None),
+                                          (range(1, k + 1), torch.cuda.Stream(cuda))]):
+        inbox.reset()
+        ser = [pickle.dumps(mlp_update(90 + 10 * rnd + j)) for j in range(k)]
+        landed = [inbox.land(s, r) for s, r in zip(ser, rows)]
+        node.received_models = [{"model": u, "sender": j} for j, u in enumerate(landed)]
+        flat = [np.concatenate([pickle.loads(s)[name].numpy().reshape(-1) for name, _ in MLP_SHAPES])
+                for s in ser]
+        want, _ = oracle.fedavg(flat, w)
+        if stream is None:
+            agg.aggregate_models(node)
+        else:
+            stream.wait_stream(torch.cuda.current_stream(cuda))
+            with torch.cuda.stream(stream):
+                agg.aggregate_models(node)
+            torch.cuda.current_stream(cuda).wait_stream(stream)
+        got = np.concatenate([t.detach().cpu().numpy().reshape(-1) for t in model.state_dict().values()])
+        assert_bits_equal(got, want, what=f"round {rnd}")
+        w = want
+    mine = [key for key in ops._TABLES if key[1:3] == (inbox.slab.data_ptr(), k + 1)]
+    assert len(mine) == 2  # one table per row set (0..3, 1..4), reused across rounds and streams
