@@ -318,7 +318,7 @@ def _many_tiles_case(rule, k):
 
 
 @pytest.mark.parametrize("rule", ["median", "trimmed"])
-@pytest.mark.parametrize("k", [100, 256])
+@pytest.mark.parametrize("k", [100, 200, 256])
 def test_robust_unaligned_views(cuda, rule, k):
     """Peer views at odd float offsets cannot be LDS-DMA'd (16-B pieces): the
     register-staged fill must give the same bits."""
@@ -336,7 +336,7 @@ def test_robust_unaligned_views(cuda, rule, k):
 
 
 @pytest.mark.parametrize("rule", ["median", "trimmed"])
-@pytest.mark.parametrize("k", [72, 256])
+@pytest.mark.parametrize("k", [72, 200, 256])
 def test_robust_segments(cuda, rule, k):
     """One launch over a state_dict of ragged tensors (segment table)."""
     sizes = [1, 15, 16, 17, 4099, 33_333, 100_000]
