@@ -25,6 +25,12 @@ Sub-records (the "sub" object of the same line):
                 -- the segment-table kernel the reference's caller reaches
   cfg4_median / cfg4_trimmed / median256 / trimmed256
                 the robust rules at 128 peers x 100M and 256 peers x 100M
+  cfg5          digest -> accept -> FedAvg over 256 serialized 100-MB updates
+                (the GPU SHA-256 batch kernel; hashlib baseline beside it)
+  delta         the trainer-side local update over 1B parameters
+  inbox         16 serialized ResNet-18 updates landed in the device slab
+                (vs the reference's pickle.loads), with the echo digest
+                overlapped
 (N = 1 only, except cfg3_full, which runs at every N.)
 
 roofline.achieved = algorithmic bytes per launch 4n(K+2) / mean kernel time
@@ -79,7 +85,8 @@ WORKLOADS = {
     # params each) in the device slab vs the reference's pickle.loads
     "inbox": ("inbox", 16, 11_689_512, 0x5EED0007),
 }
-SUB_N1 = ["cfg2-dropin", "cfg4-median", "cfg4-trimmed", "median256", "trimmed256"]
+SUB_N1 = ["cfg2-dropin", "cfg4-median", "cfg4-trimmed", "median256", "trimmed256", "cfg5", "delta", "inbox"]
+SUB_STEPS = {"cfg5": 2, "delta": 10, "inbox": 3}  # timed steps of the one-GPU sub-records
 MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
 
@@ -629,10 +636,11 @@ def run_digest_workload(args, rule, K, n, seed, dev):
             res = dict(res, value=hashed / host_s / 1e9, value_1thread=res["value_1thread"])
             what += f" + reference FedAvg ops over {acc} accepted (host, {fed['value']:.1f} GB/s)"
         cpu = cpu_record(res, "GB/s", "port", f"{what}, {res['reps']} reps in {res['seconds']}s")
-    print(json.dumps({
-        "metric": METRIC, "value": round(hashed / step_s / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u32 (SHA-256) + fp32",
+    del buf, ptrs, lens_d, digests, expected, payload_tbl, w
+    torch.cuda.empty_cache()
+    return {
+        "workload": args.workload, "value": round(hashed / step_s / 1e9, 3), "unit": "GB/s", "steps": args.steps,
+        "ms_per_step": round(step_s * 1e3, 3), "scaling": "weak", "dtype": "u32 (SHA-256) + fp32",
         "data": "synthetic serialized updates (64-B header + device-PRNG fp32 payload)",
         "config": {"workload": f"{args.workload}: {K} messages x {msg_bytes:,} B"
                                + (f", {len(bad)} corrupted, FedAvg over {acc} accepted" if rule == "fused" else ""),
@@ -646,7 +654,7 @@ def run_digest_workload(args, rule, K, n, seed, dev):
                      # 2.4 GHz, ~910 instructions per 64-B block on the chain
                      "chain_issue_bound_gbs": round(min(K, 65536) * 64 / (910 * 4 / 2.4e9) / 1e9, 2)},
         "cpu_baseline": cpu,
-    }), flush=True)
+    }
 
 
 # ------------------------------------------------------------------ delta / inbox
@@ -693,15 +701,16 @@ def run_delta_workload(args, n, seed, dev):
         res = cb.delta(n_s, args.cpu_seconds)
         cpu = cpu_record(res, "GB/s", "port", f"{n_s:,} fp32 params, reference ops cur - prev and clone "
                                               f"(node/node.py:279,282) on torch CPU, {res['reps']} reps")
-    print(json.dumps({
-        "metric": METRIC, "value": round(alg / step_s / 1e9, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+    del cur, prev, delta
+    torch.cuda.empty_cache()
+    return {
+        "workload": "delta", "value": round(alg / step_s / 1e9, 2), "unit": "GB/s", "steps": args.steps,
+        "ms_per_step": round(step_s * 1e3, 4), "scaling": "weak", "dtype": "fp32",
         "data": "synthetic (device counter PRNG); value = algorithmic bytes (16 B/param) per second",
         "config": {"workload": f"delta: trainer local update over {n:,} fp32 params (SURVEY §8(f) row 2)",
                    "coords_per_gpu": n, "parallelism": "single GPU (replicas only)"},
         "roofline": dict(roofline(alg, kern_ms, None), traffic=traffic_for("delta", n, 1)),
-        "cpu_baseline": cpu}), flush=True)
+        "cpu_baseline": cpu}
 
 
 def run_inbox_workload(args, K, n, seed, dev):
@@ -782,10 +791,12 @@ def run_inbox_workload(args, K, n, seed, dev):
     t_dig, t_seq, t_ref_dig = timed(ours_digest), timed(land_then_hash), timed(reference_echo)
     n = sum(_numel(s) for _, s in shapes)
     nbytes = K * n * 4
-    print(json.dumps({
-        "metric": METRIC, "value": round(nbytes / t_ours / 1e9, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(t_ours * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic ResNet-18 updates pickled from CUDA tensors",
+    del inbox, template
+    torch.cuda.empty_cache()
+    return {
+        "workload": "inbox", "value": round(nbytes / t_ours / 1e9, 3), "unit": "GB/s", "steps": args.steps,
+        "ms_per_step": round(t_ours * 1e3, 3), "scaling": "weak",
+        "dtype": "fp32", "data": "synthetic ResNet-18 updates pickled from CUDA tensors",
         "config": {"workload": f"inbox: land {K} serialized updates of {n:,} params ({len(shapes)} tensors) "
                                f"in the device slab (SURVEY §8(f) row 1)", "reference_pickle_loads_gbs":
                    round(nbytes / t_ref / 1e9, 3), "reference_ms": round(t_ref * 1e3, 3),
@@ -797,7 +808,21 @@ def run_inbox_workload(args, K, n, seed, dev):
                    "parallelism": "single GPU, host-to-device"},
         "roofline": {"bound": "pcie (host-to-device)", "achieved": round(nbytes / t_ours / 1e9, 2), "peak": 63.0,
                      "unit": "GB/s", "frac": round(nbytes / t_ours / 1e9 / 63.0, 4), "traffic": None},
-        "cpu_baseline": None}), flush=True)
+        "cpu_baseline": {"value": round(nbytes / t_ref / 1e9, 3), "unit": "GB/s", "kind": "reference",
+                         "cores": 1, "sample": f"the reference's own pickle.loads of the same {K} messages "
+                                               f"(node/node.py:135), same process"}}
+
+
+def replica_workload(args, name, dev):
+    """cfg5 / sha256 / delta / inbox (one GPU each): the workload's record."""
+    rule, K, n, seed = WORKLOADS[name]
+    if name == args.workload:
+        K, n = args.peers or K, args.coords or n
+    if rule in ("fused", "sha256"):
+        return run_digest_workload(args, rule, K, n, seed, dev)
+    if rule == "delta":
+        return run_delta_workload(args, n, seed, dev)
+    return run_inbox_workload(args, K, n, seed, dev)
 
 
 # ------------------------------------------------------------------ main
@@ -828,12 +853,14 @@ def main():
                "delta": "delta runs as replicas only", "inbox": "inbox runs on one GPU", "dropin": "drop-in runs on one GPU"}
     if rule in one_gpu and world > 1:
         raise SystemExit(one_gpu[rule] + " (one process per GPU)")
-    if rule in ("fused", "sha256"):
-        return run_digest_workload(args, rule, K, n, seed, dev)
-    if rule == "delta":
-        return run_delta_workload(args, n, seed, dev)
-    if rule == "inbox":
-        return run_inbox_workload(args, K, n, seed, dev)
+    if rule in ("fused", "sha256", "delta", "inbox"):
+        rec = replica_workload(args, args.workload, dev)
+        print(json.dumps({"metric": METRIC, "value": rec["value"], "unit": rec["unit"], "n_gpus": 1,
+                          "steps": rec["steps"], "warmup": args.warmup, "ms_per_step": rec["ms_per_step"],
+                          "higher_is_better": True, "scaling": rec["scaling"], "vs_baseline": None,
+                          "dtype": rec["dtype"], "data": rec["data"], "config": rec["config"],
+                          "roofline": rec["roofline"], "cpu_baseline": rec["cpu_baseline"]}), flush=True)
+        return
 
     data = "synthetic (device counter PRNG, SURVEY.md §8(d)); random-init model weights"
     if args.job == "cfg3-full":
@@ -861,6 +888,11 @@ def main():
                     r, k2, n2, s2 = WORKLOADS[name]
                     if r == "dropin":
                         rec = measure_dropin(c, args, name, k2, s2, 30, 2, args.sub_cpu_seconds)
+                    elif r in ("fused", "delta", "inbox"):
+                        sargs = argparse.Namespace(**dict(vars(args), workload=name, steps=SUB_STEPS[name],
+                                                          warmup=1, cpu_seconds=args.sub_cpu_seconds))
+                        rec = replica_workload(sargs, name, dev)
+                        rec["workload"] = name
                     else:
                         rec, _ = measure_flat(c, args, name, r, k2, n2, s2, 10, 2, args.sub_cpu_seconds, 1)
                     sub[rec["workload"]] = rec
