@@ -125,7 +125,7 @@ constexpr int kShaLanes = 64;
 __global__ __launch_bounds__(128) void sha256_pair_kernel(const uint8_t* const* __restrict__ msgs,
                                                           const uint64_t* __restrict__ lens, int k,
                                                           uint8_t* __restrict__ digests) {
-  __shared__ __attribute__((aligned(16))) u32x4 ring[2][16][kShaLanes];
+  __shared__ __attribute__((aligned(16))) u32x4 ring[3][16][kShaLanes];
   const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * kShaLanes + lane;
@@ -145,34 +145,55 @@ __global__ __launch_bounds__(128) void sha256_pair_kernel(const uint8_t* const* 
   nmax = uniform_u64(nmax);
   const bool al16 = (reinterpret_cast<uintptr_t>(m) & 15) == 0;
 
-  if (wi == 1) {  // schedule wave: block j+1 while wave 0 compresses block j
-    for (uint64_t j = 0; j < nmax; ++j) {
-      if (j < nb) {
-        uint32_t W[64];
-        load_block(W, m, len, j, al16);
-        schedule_kw(W);
+  // Three-slot ring, ONE barrier per block: before barrier j the schedule
+  // wave has expanded block j+2 (and written blocks <= j+1); after it, it
+  // stores block j+2 while the round wave issues the LDS reads of block j+1
+  // and then runs block j's rounds from registers -- the read latency hides
+  // behind 64 rounds and block j's K+W never waits on the ring.
+  auto put = [&](int slot, const uint32_t (&W)[64]) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) ring[j & 1][q][lane] = u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]};
+    for (int q = 0; q < 16; ++q) ring[slot][q][lane] = u32x4{W[4 * q], W[4 * q + 1], W[4 * q + 2], W[4 * q + 3]};
+  };
+  auto get = [&](int slot, uint32_t (&kw)[64]) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const u32x4 x = ring[slot][q][lane];
+      kw[4 * q] = x.x; kw[4 * q + 1] = x.y; kw[4 * q + 2] = x.z; kw[4 * q + 3] = x.w;
+    }
+  };
+  if (wi == 1) {  // schedule wave
+    for (uint64_t j = 0; j < 2 && j < nb; ++j) {
+      uint32_t W[64];
+      load_block(W, m, len, j, al16);
+      schedule_kw(W);
+      put(static_cast<int>(j), W);
+    }
+    __syncthreads();  // blocks 0 and 1 are in the ring
+    for (uint64_t j = 0; j < nmax; ++j) {
+      uint32_t W[64];
+      const bool more = j + 2 < nb;
+      if (more) {
+        load_block(W, m, len, j + 2, al16);
+        schedule_kw(W);
       }
-      __syncthreads();  // block j is in the ring
-      __syncthreads();  // wave 0 has read it: fill block j+1 while wave 0 compresses block j
+      __syncthreads();  // barrier j: slot (j+2)%3 (block j-1) has been read
+      if (more) put(static_cast<int>((j + 2) % 3), W);
     }
     return;
   }
   uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                    0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-  for (uint64_t j = 0; j < nmax; ++j) {
-    __syncthreads();  // block j is in the ring
-    uint32_t kw[64];
-    if (j < nb) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const u32x4 x = ring[j & 1][q][lane];
-        kw[4 * q] = x.x; kw[4 * q + 1] = x.y; kw[4 * q + 2] = x.z; kw[4 * q + 3] = x.w;
-      }
-    }
-    __syncthreads();  // slot j&1 read: wave 1 may refill it with block j+2
-    if (j < nb) rounds_kw(h, kw);
+  uint32_t kwa[64], kwb[64];
+  __syncthreads();  // blocks 0 and 1 are in the ring
+  if (nb > 0) get(0, kwa);
+  for (uint64_t j = 0; j < nmax; j += 2) {  // two blocks per trip: kwa / kwb alternate
+    __syncthreads();  // barrier j: block j+1 is in slot (j+1)%3
+    if (j + 1 < nb) get(static_cast<int>((j + 1) % 3), kwb);
+    if (j < nb) rounds_kw(h, kwa);
+    if (j + 1 >= nmax) break;
+    __syncthreads();  // barrier j+1
+    if (j + 2 < nb) get(static_cast<int>((j + 2) % 3), kwa);
+    if (j + 1 < nb) rounds_kw(h, kwb);
   }
   if (live) {
     uint4* d = reinterpret_cast<uint4*>(digests + 32 * static_cast<int64_t>(i));
