@@ -28,16 +28,21 @@ constexpr int kRobustTile = 128;  // coordinates per block (one lane each)
 
 template <int KP, int RULE, int MODE>
 __device__ __forceinline__ float robust_coord(const float* const* __restrict__ peers, int K,
-                                              int trim_b, int64_t i) {
+                                              int trim_b, int64_t c0, uint32_t lane_off) {
   // Loads are unconditional (a pad slot re-reads peer 0, an L2 hit) so the
   // compiler can keep all of them in flight: a branch around each load made
   // it wait for every load before the branch merge (serialised, ~8x slower).
+  // Each is the saddr form: the peer row's base + the tile start in SGPRs and
+  // one 32-bit lane offset shared by every load (no 64-bit VGPR address per
+  // load); the asm keeps LLVM from re-associating the tile start into it.
   uint32_t v[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
     const bool real = (MODE != 0) || (j < K);  // MODE 1/2: K == KP
-    const float* p = table_at(peers, real ? j : 0);
-    v[j] = __float_as_uint(ldg_nt(p + i));
+    uint64_t row = reinterpret_cast<uint64_t>(table_at(peers, real ? j : 0) + c0);
+    asm("" : "+s"(row));
+    v[j] = __float_as_uint(__builtin_nontemporal_load(
+        reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off)));
   }
   __builtin_amdgcn_sched_barrier(0);  // all KP loads in flight before the first use
 #pragma unroll
@@ -94,9 +99,10 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
 template <int KP, int RULE, int MODE>
 __device__ __forceinline__ void robust_one(const float* const* peers, int K, int trim_b, int64_t n,
                                            int64_t tile, float* w, float* out, float lr) {
-  const int64_t i = tile * kRobustTile + threadIdx.x;
+  const int64_t c0 = tile * kRobustTile;
+  const int64_t i = c0 + tid_x();
   if (i >= n) return;
-  const float agg = robust_coord<KP, RULE, MODE>(peers, K, trim_b, i);
+  const float agg = robust_coord<KP, RULE, MODE>(peers, K, trim_b, c0, tid_x() * 4u);
   if (out) stg(out + i, agg);
   if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
 }
@@ -105,13 +111,13 @@ template <int KP, int RULE, int MODE>
 __global__ __launch_bounds__(kRobustTile) void robust_flat_kernel(
     const float* const* __restrict__ peers, int K, int trim_b, int64_t n, float* w, float* out,
     float lr) {
-  robust_one<KP, RULE, MODE>(peers, K, trim_b, n, blockIdx.x, w, out, lr);
+  robust_one<KP, RULE, MODE>(peers, K, trim_b, n, bid_x(), w, out, lr);
 }
 
 template <int KP, int RULE, int MODE>
 __global__ __launch_bounds__(kRobustTile) void robust_segments_kernel(
     const Seg* __restrict__ segs, int nseg, int K, int trim_b, float lr) {
-  const int64_t t = blockIdx.x;
+  const int64_t t = bid_x();
   const Seg s = load_segment(segs, nseg, t);
   robust_one<KP, RULE, MODE>(s.peers, K, trim_b, s.n, t - s.tile_begin, s.w, s.out, lr);
 }

@@ -59,6 +59,10 @@ __device__ __forceinline__ u16x2 pmax(u16x2 a, u16x2 b) { return __builtin_eleme
 #ifndef P2P_NO_FLOAT_PATH
 #define P2P_NO_FLOAT_PATH 0
 #endif
+// A/B build only (make nopair): K = 256 on the 4-lane kernel, not robust_pair.hip.
+#ifndef P2P_NO_PAIR
+#define P2P_NO_PAIR 0
+#endif
 
 namespace p2p {
 
@@ -365,7 +369,7 @@ __device__ __forceinline__ void radix_median_pair(uint32_t (&ka)[64], uint32_t (
     rb = __uint_as_float(key2f(ub + lb));
   } else {  // valid in lane q == 0 either way
 #ifdef P2P_LAB
-    atomicAdd(&g_lab_fallback[threadIdx.x & 63], 1);  // per-lane slots: a vector atomic
+    atomicAdd(&g_lab_fallback[tid_x() & 63], 1);  // per-lane slots: a vector atomic
 #endif
     bool own = false;
     ra = reduce_keys<4, 64, P2P_RULE_MEDIAN, 1>(ka, q, 256, 0, own);
@@ -439,15 +443,15 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
   static_assert(PK == 1 || (L == 4 && H == 64 && RULE == P2P_RULE_MEDIAN && MODE == 1), "radix16: median of 256");
   __shared__ __attribute__((aligned(16))) uint8_t lds_raw[Lay::BYTES];
   uint8_t P2P_LDS* lds = (uint8_t P2P_LDS*)lds_raw;
-  const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
+  const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
+  const int lane = tid_x() & 63;
   const bool loader = wi >= Lay::W;  // wave-uniform role
   const int li = wi - Lay::W;        // loader index
   const int q = lane % L, c = wi * Lay::TW + lane / L;  // sorters: coordinate inside the block tile
 
-  const int64_t nb = gridDim.x;
-  int64_t t = blockIdx.x;
-  if ((nb & 7) == 0) t = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);  // XCD-contiguous tiles
+  const int64_t nb = nblocks_x();
+  int64_t t = bid_x();
+  if ((nb & 7) == 0) t = (bid_x() & 7) * (nb >> 3) + (bid_x() >> 3);  // XCD-contiguous tiles
   if (t >= ntiles) return;
 
   // loaders: per-lane row pointers of their DMA pieces for the bound source.
@@ -655,16 +659,16 @@ __global__ __launch_bounds__(768) void robust_lds_g2_kernel(const float* const* 
   static_assert(Lay::NBUF == 2 && Lay::W == 4, "one image per sorter group");
   __shared__ __attribute__((aligned(16))) uint8_t lds_raw[Lay::BYTES];
   uint8_t P2P_LDS* lds = (uint8_t P2P_LDS*)lds_raw;
-  const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
+  const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
+  const int lane = tid_x() & 63;
   const bool loader = wi >= 2 * Lay::W;  // wave-uniform role
   const int g = loader ? 0 : wi / Lay::W;
   const int li = wi - 2 * Lay::W;
   const int q = lane % L, c = (wi % Lay::W) * Lay::TW + lane / L;
 
-  const int64_t nb = gridDim.x;
-  int64_t t0 = blockIdx.x;
-  if ((nb & 7) == 0) t0 = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);  // XCD-contiguous tiles
+  const int64_t nb = nblocks_x();
+  int64_t t0 = bid_x();
+  if ((nb & 7) == 0) t0 = (bid_x() & 7) * (nb >> 3) + (bid_x() >> 3);  // XCD-contiguous tiles
   if (t0 >= ntiles) return;  // block-uniform
   const int64_t iters = ceil_div(ceil_div(ntiles - t0, nb), 2);
   auto tile_at = [&](int64_t i, int gg) { return t0 + (2 * i + gg) * nb; };
@@ -854,8 +858,13 @@ extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t rule, int32_t k) {
   return LdsLayout<4, 64>::TB;
 }
 
-// K = 256 with the default trim (the pruned networks, float fast path): one
-// sorter group per block.  Any other K in 129..255 or trim runs the generic
+extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, const p2p_segment_t* segs,
+                                                    int32_t nseg, int64_t tiles, int32_t rule, int64_t n,
+                                                    float* w, float* out, float lr, p2p_stream_t stream);
+
+// K = 256 with the default trim (the pruned networks): one lane per
+// coordinate in two-wave blocks, robust_pair.hip (A/B build P2P_NO_PAIR: the
+// 4-lane kernel above, one sorter group per block).  Any other K in 129..255 or trim runs the generic
 // padded network -- ~1.4x the instructions -- where two sorter groups per
 // block are faster (median -7%, trimmed -12% time for K in 129..255, round-2
 // lab A/B, profiles/r02/ab/labg2k); for the pruned K = 256 networks the
@@ -868,8 +877,12 @@ extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, co
   const bool med = rule == P2P_RULE_MEDIAN;
   const bool pruned = k == 256 && (med || trim_b == (256 * 2) / 10);
   if (pruned) {
+#if P2P_NO_PAIR
     if (med) launch_lds_mode<4, 64, P2P_RULE_MEDIAN, 1, 0>(a);
     else launch_lds_mode<4, 64, P2P_RULE_TRIMMED, 2, 0>(a);
+#else
+    p2p_robust_pair_launch(peers, segs, nseg, tiles, rule, n, w, out, lr, stream);
+#endif
   } else if (med) {
     if (segs) launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, true>(a); else launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, false>(a);
   } else {

@@ -1,0 +1,277 @@
+// K2 at K = 256 with the pruned rules (median; trimmed mean with b = 51):
+// ONE lane per coordinate, a block of two waves over 64 coordinates.
+//
+// Rule (no reference implementation, README.md:10):
+//   median : key of rank 127 under the IEEE total order on float bits
+//   trimmed: fp32 sum of ranks 51..204 ascending from +0, IEEE-divided by 154
+// then w += lr*agg, multiply and add separately rounded (aggregation.py:36-38).
+//
+// Wave h loads peers 128h..128h+127 of its 64 coordinates (every load
+// instruction reads 256 contiguous bytes of one peer) and sorts them in
+// VGPRs with Batcher's 128-key network -- half A (h = 0) and half B (h = 1).
+// Wave 0 hands its sorted A to wave 1 through LDS (32 KB: four keys per lane
+// per ds_write_b128), and the two sorted halves meet in one flip:
+//   L_j = min(B_j, A_{127-j}),  U_j = max(B_j, A_{127-j})   (j = 0..127)
+// L is the 128 smallest keys of the coordinate, U the 128 largest, each a
+// bitonic sequence.
+//   median : rank 127 = max_j L_j -- wave 1 finishes with 128 v_min and 64
+//            v_max3, no merge at all.
+//   trimmed: wave 1 writes U back over A in LDS; wave 1 merges L pruned to
+//            ranks 51..127, wave 0 merges U pruned to ranks 0..76, and the
+//            ascending sum runs over L's ranks in wave 1 and carries on over
+//            U's in wave 0 (the partial sum crosses through LDS).
+// Against the 4-lanes-per-coordinate LDS kernel this issues ~10% (median) /
+// ~22% (trimmed) fewer VALU instructions per coordinate -- two 128-key sorts
+// instead of four 64-key sorts plus cross-lane bitonic merges, no DPP moves,
+// and the trimmed sum advances 64 coordinates per instruction instead of 16 --
+// and no wave only loads: every wave sorts, 2 per SIMD (≤ 256 VGPRs; 32 KB of
+// LDS per block, 4 blocks per CU), each hiding the other's HBM latency.
+//
+// Float or key network, per block: the two waves swap a "my half holds a
+// NaN" flag through LDS; without one the block sorts the float values
+// themselves (robust_nets.h: same order, same bits as the uint32 keys),
+// otherwise uint32 total-order keys.  The key path is out of line and
+// re-loads its inputs (pair_keys): inlined next to the float path, LLVM kept
+// both paths' 128 values live and the kernel took 320-390 VGPRs.
+#include "robust_nets.h"
+
+namespace p2p {
+
+constexpr int kPairTile = 64;  // coordinates per block, one lane each
+constexpr int kHalf = 128;     // peers per wave
+
+__device__ __forceinline__ float val(fk x) { return x.x; }
+__device__ __forceinline__ uint32_t raw(fk x) { return __float_as_uint(x.x); }
+__device__ __forceinline__ uint32_t raw(uint32_t k) { return k; }
+__device__ __forceinline__ float val(uint32_t k) { return __uint_as_float(key2f(k)); }
+template <typename T> __device__ __forceinline__ T from_bits(uint32_t b);
+template <> __device__ __forceinline__ fk from_bits<fk>(uint32_t b) { return fk{__uint_as_float(b)}; }
+template <> __device__ __forceinline__ uint32_t from_bits<uint32_t>(uint32_t b) { return f2key(b); }
+// An element as it crosses LDS: the T-domain word itself (float bits or key).
+template <typename T> __device__ __forceinline__ T from_raw(uint32_t b);
+template <> __device__ __forceinline__ fk from_raw<fk>(uint32_t b) { return fk{__uint_as_float(b)}; }
+template <> __device__ __forceinline__ uint32_t from_raw<uint32_t>(uint32_t b) { return b; }
+
+// LDS image of one sorted half: element j of lane l at word (j & 3) of
+// slot [j >> 2][l] -- 1 KiB per ds_write_b128 / ds_read_b128, no bank conflict.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Image slots read ahead of their use: the compiler would otherwise issue all
+// 32 reads at once (and hold the other half in 128 more VGPRs).  fence_after
+// makes a result computed from the slots read so far an input of a
+// memory-clobbering asm, so neither that arithmetic sinks below nor later
+// reads rise above it.
+constexpr int kReadAhead = 4;
+template <typename T>
+__device__ __forceinline__ void fence_after(T& x) {
+  uint32_t r = raw(x);
+  asm volatile("" : "+v"(r)::"memory");
+  x = from_raw<T>(r);
+}
+using Img = u32x4 __attribute__((address_space(3)))*;
+
+__device__ __forceinline__ uint32_t img_at(Img im, int j, int lane) { return im[(j >> 2) * 64 + lane][j & 3]; }
+
+// A wave-uniform flag the compiler also KNOWS is uniform: an inline-asm SGPR
+// result counts as divergent, and a branch on it is linearised -- both the
+// float and the key network then run under exec masks with the inputs live
+// across both (376 VGPRs instead of ~200).
+__device__ __forceinline__ bool uniform(bool x) {
+  return __builtin_amdgcn_readfirstlane(static_cast<int>(x)) != 0;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_half(Img im, const T (&x)[kHalf], int lane) {
+#pragma unroll
+  for (int g = 0; g < kHalf / 4; ++g)
+    im[g * 64 + lane] = u32x4{raw(x[4 * g]), raw(x[4 * g + 1]), raw(x[4 * g + 2]), raw(x[4 * g + 3])};
+}
+
+// median: max_j min(B_j, A_{127-j}), A read from the image in T's domain.
+template <typename T>
+__device__ __forceinline__ float median_final(Img im, const T (&b)[kHalf], int lane) {
+  T m{};
+#pragma unroll
+  for (int g = 0; g < kHalf / 4; ++g) {
+    const u32x4 a4 = im[(kHalf / 4 - 1 - g) * 64 + lane];  // A_{127-4g-k} = word 3-k
+    const T l0 = min(b[4 * g], from_raw<T>(a4[3])), l1 = min(b[4 * g + 1], from_raw<T>(a4[2]));
+    const T l2 = min(b[4 * g + 2], from_raw<T>(a4[1])), l3 = min(b[4 * g + 3], from_raw<T>(a4[0]));
+    const T q = max(max(l0, l1), max(l2, l3));
+    m = g == 0 ? q : max(m, q);
+    if (g % kReadAhead == kReadAhead - 1) fence_after(m);  // bound the reads in flight
+  }
+  return val(m);
+}
+
+// trimmed, wave 1: L_j = min(B_j, A_{127-j}) stays in b; U_j = max(...) is
+// written over A_{127-j}'s word (each slot is read before it is rewritten).
+template <typename T>
+__device__ __forceinline__ void flip_write_upper(Img im, T (&b)[kHalf], int lane) {
+#pragma unroll
+  for (int g = 0; g < kHalf / 4; ++g) {
+    const int s = (kHalf / 4 - 1 - g) * 64 + lane;
+    const u32x4 a4 = im[s];
+    u32x4 u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const T a = from_raw<T>(a4[3 - k]);
+      const T lo = min(b[4 * g + k], a), hi = max(b[4 * g + k], a);
+      b[4 * g + k] = lo;
+      u[3 - k] = raw(hi);
+    }
+    im[s] = u;
+    if (g % kReadAhead == kReadAhead - 1) fence_after(b[4 * g + 3]);
+  }
+}
+
+// Sum of ranks [R0, R1) of a merged half, ascending, continuing from acc.
+template <int R0, int R1, typename T>
+__device__ __forceinline__ float sum_ranks(const T (&x)[kHalf], float acc) {
+#pragma unroll
+  for (int j = R0; j < R1; ++j) acc = __fadd_rn(acc, val(x[j]));
+  return acc;
+}
+
+__device__ __forceinline__ void block_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Pins a sorted half where it is computed.  Without a use on both sides of
+// the role branches LLVM sinks the network into one successor piecemeal, which
+// scrambles its order (a 128-key sort then holds ~250 VGPRs instead of ~135).
+template <typename T>
+__device__ __forceinline__ void pin(const T (&x)[kHalf]) {
+#pragma unroll
+  for (int j = 0; j < kHalf; ++j) asm volatile("" ::"v"(raw(x[j])));
+}
+
+// One half sorted in T's domain (the block's: keys if either half holds a
+// NaN); returns the aggregate, valid where `own`.  Both waves pass the same
+// number of block barriers.
+template <int RULE, typename T>
+__device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, int h, int lane) {
+  T x[kHalf];
+#pragma unroll
+  for (int j = 0; j < kHalf; ++j) x[j] = from_bits<T>(v[j]);
+  sort_full<kHalf>(x);
+  pin(x);
+  if (h == 0) store_half(im, x, lane);
+  block_sync();  // 1: A in the image
+  if constexpr (RULE == P2P_RULE_MEDIAN) {
+    return h == 1 ? median_final(im, x, lane) : 0.f;
+  } else {
+    constexpr int b = (2 * kHalf * 2) / 10;  // 51
+    constexpr int hi = 2 * kHalf - b;        // 205: ranks b..hi-1 kept
+    auto part = (float __attribute__((address_space(3)))*)im;
+    if (h == 1) {
+      flip_write_upper(im, x, lane);
+      block_sync();  // 2: U_j in A_{127-j}'s word
+      net_bmerge128_r51_127<true>(x);
+      block_sync();  // 3: wave 0 has read U
+      part[lane] = sum_ranks<b, kHalf>(x, 0.f);
+      block_sync();  // 4: the partial sum of ranks 51..127 in the image
+      return 0.f;
+    }
+    block_sync();  // 2
+#pragma unroll
+    for (int j = 0; j < kHalf; ++j) x[j] = from_raw<T>(img_at(im, kHalf - 1 - j, lane));
+    net_bmerge128_r0_76<true>(x);
+    block_sync();  // 3
+    block_sync();  // 4
+    return sum_ranks<0, hi - kHalf>(x, part[lane]) / static_cast<float>(hi - b);
+  }
+}
+
+// This wave's 128 inputs of the tile.  Every load is the saddr form: the
+// peer row's base plus the tile start in SGPRs, one 32-bit lane offset shared
+// by all 128 loads -- no 64-bit VGPR address per load.  The asm keeps LLVM
+// from re-associating the tile start into the lane offset.
+__device__ __forceinline__ void load_half(uint32_t (&v)[kHalf], const float* const* P, int64_t c0,
+                                          uint32_t lane_off, int h) {
+#pragma unroll
+  for (int j = 0; j < kHalf; ++j) {
+    uint64_t row = reinterpret_cast<uint64_t>(table_at(P, h * kHalf + j) + c0);
+    asm("" : "+s"(row));
+    v[j] = __float_as_uint(__builtin_nontemporal_load(
+        reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off)));
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first use
+}
+
+// The uint32-key network for a block holding a NaN.  Out of line and
+// re-loading its inputs, so the float path's 128 values are not also held
+// live for this one (inlined, the two paths took 320-390 VGPRs).
+template <int RULE>
+__device__ __attribute__((noinline)) float pair_keys(const float* const* P, int64_t c0, uint32_t lane_off, Img im,
+                                                     int h, int lane) {
+  // arguments arrive in VGPRs: make the wave-uniform ones scalar again
+  P = reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(P)));
+  c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(c0)));
+  h = __builtin_amdgcn_readfirstlane(h);
+  uint32_t v[kHalf];
+  load_half(v, P, c0, lane_off, h);
+  return pair_body<RULE, uint32_t>(v, im, h, lane);
+}
+
+template <int RULE, bool SEGS>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(const float* const* __restrict__ peers,
+                                                          const Seg* __restrict__ segs, int nseg, int64_t n,
+                                                          float* w, float* out, float lr) {
+  __shared__ u32x4 img_raw[kHalf / 4 * 64];  // 32 KB
+  __shared__ int nan_flag[2];
+  Img im = (Img)img_raw;
+  const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
+  const int lane = tid_x() & 63;
+  const int64_t t = bid_x();
+  const float* const* P = peers;
+  float* W = w;
+  float* O = out;
+  int64_t N = n, c0 = t * kPairTile;
+  if constexpr (SEGS) {
+    const Seg s = load_segment(segs, nseg, t);
+    P = s.peers;
+    W = s.w;
+    O = s.out;
+    N = s.n;
+    c0 = (t - s.tile_begin) * kPairTile;
+  }
+  const int64_t i = c0 + lane;
+  // Dead lanes of a ragged tail re-read the last element.
+  const uint32_t lane_off = static_cast<uint32_t>((i < N ? i : N - 1) - c0) * 4u;
+  uint32_t v[kHalf];
+  load_half(v, P, c0, lane_off, h);
+  // One domain per block: the float network unless either half holds a NaN.
+  const bool nan = uniform(wave_has_nan(v));
+  if (lane == 0) nan_flag[h] = nan ? 1 : 0;
+  block_sync();
+  const bool keys = uniform((nan_flag[0] | nan_flag[1]) != 0);
+  const float agg = keys ? pair_keys<RULE>(P, c0, lane_off, im, h, lane) : pair_body<RULE, fk>(v, im, h, lane);
+  const bool own = RULE == P2P_RULE_MEDIAN ? h == 1 : h == 0;
+  if (own && i < N) {
+    if (O) stg(O + i, agg);
+    if (W) stg(W + i, apply_lr(ldg(W + i), lr, agg));
+  }
+}
+
+}  // namespace p2p
+
+using namespace p2p;
+
+// K = 256, median or trimmed with b = 51: grid = one block per 64-coordinate
+// tile (flat: ceil(n / 64); segment table: `tiles`, tile_begin in units of 64).
+extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, const p2p_segment_t* segs,
+                                                    int32_t nseg, int64_t tiles, int32_t rule, int64_t n,
+                                                    float* w, float* out, float lr, p2p_stream_t stream) {
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t grid = segs ? tiles : ceil_div(n, kPairTile);
+  if (grid <= 0) return;
+  const dim3 g(static_cast<unsigned>(grid)), b(2 * 64);
+  if (rule == P2P_RULE_MEDIAN) {
+    if (segs) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    else hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+  } else {
+    if (segs) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    else hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+  }
+}
