@@ -224,6 +224,18 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
   const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
   const int lane = tid_x() & 63;
   const int64_t t = bid_x();
+#ifdef P2P_PAIR_STAGGER
+  // lab: start some first-round blocks half a block period late, so the two
+  // waves sharing a SIMD load and sort out of phase
+  {
+    const uint32_t b = bid_x();
+    const bool late = b < 2048 && (P2P_PAIR_STAGGER == 1 ? ((b >> 8) & 2) : P2P_PAIR_STAGGER == 2 ? ((b >> 3) & 1) : ((b >> 8) & 1));
+    if (late) {
+#pragma unroll 1
+      for (int k = 0; k < P2P_PAIR_SLEEPS; ++k) __builtin_amdgcn_s_sleep(127);
+    }
+  }
+#endif
   const float* const* P = peers;
   float* W = w;
   float* O = out;
