@@ -252,7 +252,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
   // Dead lanes of a ragged tail re-read the last element.
   const uint32_t lane_off = static_cast<uint32_t>((i < N ? i : N - 1) - c0) * 4u;
   uint32_t v[kHalf];
+#if defined(P2P_PAIR_DIAG) && P2P_PAIR_DIAG == 1
+  load_half(v, P, 0, lane_off, h);  // lab: every block reads tile 0 (L2-resident): no HBM latency
+#else
   load_half(v, P, c0, lane_off, h);
+#endif
   // One domain per block: the float network unless either half holds a NaN.
   const bool nan = uniform(wave_has_nan(v));
   if (lane == 0) nan_flag[h] = nan ? 1 : 0;
