@@ -56,19 +56,14 @@ __device__ __forceinline__ T* table_at(T* const* table, int k) {
   return reinterpret_cast<T*>(((const P2P_CONST uint64_t*)(table))[k]);
 }
 
-// Work-item / work-group ids and the grid size as intrinsics.  The robust
+// Work-item / work-group ids as intrinsics (the grid size is a kernel
+// argument where a loop strides by it).  The robust
 // kernels are built with -mno-amdgpu-ieee, which keeps the device library's
-// threadIdx / blockIdx / gridDim helpers (__ockl_get_*, built IEEE) from
+// threadIdx / blockIdx helpers (__ockl_get_*, built IEEE) from
 // inlining: each became a call returning a VGPR, so block-uniform values --
 // tile bases, peer row addresses -- were computed per lane as if divergent.
 __device__ __forceinline__ uint32_t tid_x() { return __builtin_amdgcn_workitem_id_x(); }
 __device__ __forceinline__ uint32_t bid_x() { return __builtin_amdgcn_workgroup_id_x(); }
-__device__ __forceinline__ uint32_t nblocks_x() {
-  const P2P_CONST uint32_t* dp = (const P2P_CONST uint32_t*)__builtin_amdgcn_dispatch_ptr();
-  const uint32_t grid = dp[3];                                   // grid_size_x (work-items)
-  const uint32_t wg = ((const P2P_CONST uint16_t*)dp)[2];        // workgroup_size_x
-  return (grid + wg - 1) / wg;
-}
 
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));

@@ -437,7 +437,7 @@ template <int L, int H, int RULE, int MODE, bool SEGS, int NB, int PK = 1>
 __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __restrict__ peers,
                                                              const Seg* __restrict__ segs, int nseg,
                                                              int64_t ntiles, int K, int trim_b, int64_t n,
-                                                             float* w, float* out, float lr) {
+                                                             float* w, float* out, float lr, int64_t nb) {
   using Lay = LdsLayout<L, H, NB, PK>;
   static_assert(128 * Lay::W == 512, "launch bounds");
   static_assert(PK == 1 || (L == 4 && H == 64 && RULE == P2P_RULE_MEDIAN && MODE == 1), "radix16: median of 256");
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
   const int li = wi - Lay::W;        // loader index
   const int q = lane % L, c = wi * Lay::TW + lane / L;  // sorters: coordinate inside the block tile
 
-  const int64_t nb = nblocks_x();
+  // nb: the grid size, passed by the launch (the persistent loop strides by it)
   int64_t t = bid_x();
   if ((nb & 7) == 0) t = (bid_x() & 7) * (nb >> 3) + (bid_x() >> 3);  // XCD-contiguous tiles
   if (t >= ntiles) return;
@@ -653,7 +653,7 @@ template <int RULE, int MODE, bool SEGS>
 __global__ __launch_bounds__(768) void robust_lds_g2_kernel(const float* const* __restrict__ peers,
                                                             const Seg* __restrict__ segs, int nseg,
                                                             int64_t ntiles, int K, int trim_b, int64_t n,
-                                                            float* w, float* out, float lr) {
+                                                            float* w, float* out, float lr, int64_t nb) {
   constexpr int L = 4, H = 64;
   using Lay = LdsLayout<L, H>;
   static_assert(Lay::NBUF == 2 && Lay::W == 4, "one image per sorter group");
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(768) void robust_lds_g2_kernel(const float* const* 
   const int li = wi - 2 * Lay::W;
   const int q = lane % L, c = (wi % Lay::W) * Lay::TW + lane / L;
 
-  const int64_t nb = nblocks_x();
+  // nb: the grid size, passed by the launch (the persistent loop strides by it)
   int64_t t0 = bid_x();
   if ((nb & 7) == 0) t0 = (bid_x() & 7) * (nb >> 3) + (bid_x() >> 3);  // XCD-contiguous tiles
   if (t0 >= ntiles) return;  // block-uniform
@@ -792,7 +792,7 @@ static void launch_lds_kernel(const LdsArgs& a) {
   const int64_t ntiles = SEGS ? a.tiles : ceil_div(a.n, Lay::TB);
   const int64_t grid = ntiles < resident ? ntiles : resident;
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, a.stream, a.peers, a.segs, a.nseg,
-                     ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
+                     ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr, grid);
 }
 
 template <int RULE, int MODE, bool SEGS>
@@ -810,7 +810,7 @@ static void launch_lds_g2_kernel(const LdsArgs& a) {
   const int64_t ntiles = SEGS ? a.tiles : ceil_div(a.n, Lay::TB);
   const int64_t grid = ntiles < resident ? ntiles : resident;
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(768), 0, a.stream, a.peers, a.segs, a.nseg,
-                     ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
+                     ntiles, a.K, a.trim_b, a.n, a.w, a.out, a.lr, grid);
 }
 
 template <int RULE>

@@ -1,3 +1,4 @@
+// LAB ONLY (tools/): persistent K = 256 pair kernel with the next tile prefetched -- hangs on multi-tile grids, under investigation; not in the product library.
 // K2 at K = 256 with the pruned rules (median; trimmed mean with b = 51):
 // ONE lane per coordinate, a block of two waves over 64 coordinates.
 //
@@ -189,14 +190,20 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
 // from re-associating the tile start into the lane offset.
 __device__ __forceinline__ void load_half(uint32_t (&v)[kHalf], const float* const* P, int64_t c0,
                                           uint32_t lane_off, int h) {
+  // opaque per call: in the persistent loop the 128 row pointers of a flat
+  // buffer are loop-invariant, and LLVM hoisted them (256 SGPRs, spilled)
+  asm volatile("" : "+s"(P));
+  asm volatile("" : "+v"(lane_off));  // a local 32-bit value: the loads take the saddr form
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) {
     uint64_t row = reinterpret_cast<uint64_t>(table_at(P, h * kHalf + j) + c0);
     asm("" : "+s"(row));
     v[j] = __float_as_uint(__builtin_nontemporal_load(
         reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off)));
+    // 8 row bases at a time: hoisted together, 128 bases (256 SGPRs) spilled
+    // into VGPR lanes (v_writelane / v_readlane) in the persistent kernel
+    if (j % 8 == 7) __builtin_amdgcn_sched_barrier(0);
   }
-  __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first use
 }
 
 // The uint32-key network for a block holding a NaN.  Out of line and
@@ -214,43 +221,94 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
   return pair_body<RULE, uint32_t>(v, im, h, lane);
 }
 
-template <int RULE, bool SEGS>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(const float* const* __restrict__ peers,
-                                                          const Seg* __restrict__ segs, int nseg, int64_t n,
-                                                          float* w, float* out, float lr) {
-  __shared__ u32x4 img_raw[kHalf / 4 * 64];  // 32 KB
-  __shared__ int nan_flag[2];
-  Img im = (Img)img_raw;
-  const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
-  const int lane = tid_x() & 63;
-  const int64_t t = bid_x();
-  const float* const* P = peers;
-  float* W = w;
-  float* O = out;
-  int64_t N = n, c0 = t * kPairTile;
+// One 64-coordinate tile: a flat buffer's or one segment's.
+struct PairTile {
+  const float* const* P;
+  float* W;
+  float* O;
+  int64_t N, c0;
+};
+
+template <bool SEGS>
+__device__ __forceinline__ PairTile pair_tile(const float* const* peers, const Seg* segs, int nseg, int64_t n,
+                                              float* w, float* out, int64_t t) {
   if constexpr (SEGS) {
     const Seg s = load_segment(segs, nseg, t);
-    P = s.peers;
-    W = s.w;
-    O = s.out;
-    N = s.n;
-    c0 = (t - s.tile_begin) * kPairTile;
+    return PairTile{s.peers, s.w, s.out, s.n, (t - s.tile_begin) * kPairTile};
+  } else {
+    return PairTile{peers, w, out, n, t * kPairTile};
   }
-  const int64_t i = c0 + lane;
-  // Dead lanes of a ragged tail re-read the last element.
-  const uint32_t lane_off = static_cast<uint32_t>((i < N ? i : N - 1) - c0) * 4u;
+}
+
+// Dead lanes of a ragged tail re-read the last element.
+__device__ __forceinline__ uint32_t lane_offset(const PairTile& T, int lane) {
+  const int64_t i = T.c0 + lane;
+  return static_cast<uint32_t>((i < T.N ? i : T.N - 1) - T.c0) * 4u;
+}
+
+// A tile's inputs for this wave: the weight first (the owner wave only), so
+// waiting for it never waits for the 128 peer loads issued after it.
+template <int RULE>
+__device__ __forceinline__ void load_tile(uint32_t (&v)[kHalf], float& wv, const PairTile& T, int h, int lane) {
+  const uint32_t off = lane_offset(T, lane);
+  wv = 0.f;
+  if (h == (RULE == P2P_RULE_MEDIAN ? 1 : 0) && T.W)
+    wv = __builtin_nontemporal_load((const P2P_GLOBAL float*)((const P2P_GLOBAL char*)(T.W + T.c0) + off));
+  load_half(v, T.P, T.c0, off, h);
+}
+
+// Persistent blocks of two waves walk tiles t, t + grid, ...; while a tile is
+// sorted, the next tile's 128 loads per wave are already in flight (the
+// registers they land in are the sort's second bank: up to 512 per wave, one
+// wave per SIMD).  Without it each wave loaded, then sorted: streaming alone
+// runs at 76% of HBM peak and the sort alone at ~68%, but the two phases of
+// the two waves sharing a SIMD barely overlapped (median256 56%,
+// profiles/r02/lab_pair).  Hand-off images and NaN flags are double-buffered
+// by tile parity, so a wave may start tile t+1 while its partner finishes t.
+template <int RULE, bool SEGS>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void robust_pair_kernel(
+    const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t ntiles, int64_t n,
+    float* w, float* out, float lr, int64_t G) {
+  __shared__ u32x4 img_raw[2][kHalf / 4 * 64];  // 2 x 32 KB
+  __shared__ int nan_flag[2][2];
+  const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
+  const int lane = tid_x() & 63;
+  int64_t t = bid_x();
+  if (t >= ntiles) return;  // block-uniform
+  PairTile T = pair_tile<SEGS>(peers, segs, nseg, n, w, out, t);
   uint32_t v[kHalf];
-  load_half(v, P, c0, lane_off, h);
-  // One domain per block: the float network unless either half holds a NaN.
-  const bool nan = uniform(wave_has_nan(v));
-  if (lane == 0) nan_flag[h] = nan ? 1 : 0;
-  block_sync();
-  const bool keys = uniform((nan_flag[0] | nan_flag[1]) != 0);
-  const float agg = keys ? pair_keys<RULE>(P, c0, lane_off, im, h, lane) : pair_body<RULE, fk>(v, im, h, lane);
-  const bool own = RULE == P2P_RULE_MEDIAN ? h == 1 : h == 0;
-  if (own && i < N) {
-    if (O) stg(O + i, agg);
-    if (W) stg(W + i, apply_lr(ldg(W + i), lr, agg));
+  float wv;
+  load_tile<RULE>(v, wv, T, h, lane);
+  const bool owner = h == (RULE == P2P_RULE_MEDIAN ? 1 : 0);
+#pragma unroll 1
+  for (int it = 0;; ++it) {
+    Img im = (Img)img_raw[it & 1];
+    // One domain per block and tile: the float network unless either half holds a NaN.
+    const bool nan = uniform(wave_has_nan(v));
+    if (lane == 0) nan_flag[it & 1][h] = nan ? 1 : 0;
+    block_sync();
+    const bool keys = uniform((nan_flag[it & 1][0] | nan_flag[it & 1][1]) != 0);
+    const int64_t tn = t + G;
+    const bool more = tn < ntiles;  // block-uniform
+    PairTile Tn = T;
+    uint32_t nv[kHalf];
+    float nwv = 0.f;
+    if (more) {
+      Tn = pair_tile<SEGS>(peers, segs, nseg, n, w, out, tn);
+      load_tile<RULE>(nv, nwv, Tn, h, lane);
+    }
+    const float agg = keys ? pair_keys<RULE>(T.P, T.c0, lane_offset(T, lane), im, h, lane)
+                           : pair_body<RULE, fk>(v, im, h, lane);
+    const int64_t i = T.c0 + lane;
+    if (owner && i < T.N) {
+      if (T.O) stg(T.O + i, agg);
+      if (T.W) stg(T.W + i, apply_lr(wv, lr, agg));
+    }
+    if (!more) break;
+    T = Tn;
+    wv = nwv;
+#pragma unroll
+    for (int j = 0; j < kHalf; ++j) v[j] = nv[j];
   }
 }
 
@@ -260,18 +318,36 @@ using namespace p2p;
 
 // K = 256, median or trimmed with b = 51: grid = one block per 64-coordinate
 // tile (flat: ceil(n / 64); segment table: `tiles`, tile_begin in units of 64).
+template <int RULE, bool SEGS>
+static void launch_pair(const float* const* peers, const p2p_segment_t* segs, int32_t nseg, int64_t ntiles,
+                        int64_t n, float* w, float* out, float lr, hipStream_t st) {
+  auto kern = robust_pair_kernel<RULE, SEGS>;
+  static int resident = 0;  // persistent grid: every resident block slot once
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 128, 0);
+    resident = (cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+  }
+  const int64_t grid = ntiles < resident ? ntiles : resident;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(128), 0, st, peers, segs, nseg, ntiles, n, w,
+                     out, lr, grid);
+}
+
+// K = 256, median or trimmed with b = 51: 64-coordinate tiles (flat:
+// ceil(n / 64); segment table: `tiles`, tile_begin in units of 64).
 extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, const p2p_segment_t* segs,
                                                     int32_t nseg, int64_t tiles, int32_t rule, int64_t n,
                                                     float* w, float* out, float lr, p2p_stream_t stream) {
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  const int64_t grid = segs ? tiles : ceil_div(n, kPairTile);
-  if (grid <= 0) return;
-  const dim3 g(static_cast<unsigned>(grid)), b(2 * 64);
+  const int64_t ntiles = segs ? tiles : ceil_div(n, kPairTile);
+  if (ntiles <= 0) return;
   if (rule == P2P_RULE_MEDIAN) {
-    if (segs) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    if (segs) launch_pair<P2P_RULE_MEDIAN, true>(peers, segs, nseg, ntiles, n, w, out, lr, st);
+    else launch_pair<P2P_RULE_MEDIAN, false>(peers, segs, nseg, ntiles, n, w, out, lr, st);
   } else {
-    if (segs) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    if (segs) launch_pair<P2P_RULE_TRIMMED, true>(peers, segs, nseg, ntiles, n, w, out, lr, st);
+    else launch_pair<P2P_RULE_TRIMMED, false>(peers, segs, nseg, ntiles, n, w, out, lr, st);
   }
 }
