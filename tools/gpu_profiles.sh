@@ -40,8 +40,8 @@ cfg3-chunk:fedavg_flat_kernel:15625000:256:--job cfg3-full --steps 1
 cfg2-dropin:fedavg_segments_kernel:11689512:64:--workload cfg2-dropin
 cfg4-median:robust_flat_kernel:100000000:128:--workload cfg4-median
 cfg4-trimmed:robust_flat_kernel:100000000:128:--workload cfg4-trimmed
-median256:robust_lds_kernel:100000000:256:--workload median256
-trimmed256:robust_lds_kernel:100000000:256:--workload trimmed256
+median256:robust_pair_kernel:100000000:256:--workload median256
+trimmed256:robust_pair_kernel:100000000:256:--workload trimmed256
 EOS
 
 # issue / wait / clock counters of the K = 256 robust kernels (8 SQ + 2 GRBM slots)
