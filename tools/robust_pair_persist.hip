@@ -1,4 +1,4 @@
-// LAB ONLY (tools/): persistent K = 256 pair kernel with the next tile prefetched -- hangs on multi-tile grids, under investigation; not in the product library.
+// LAB (tools/): persistent K = 256 pair kernel with the next tile prefetched (A/B against the product pair kernel).
 // K2 at K = 256 with the pruned rules (median; trimmed mean with b = 51):
 // ONE lane per coordinate, a block of two waves over 64 coordinates.
 //
@@ -305,6 +305,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void r
       if (T.W) stg(T.W + i, apply_lr(wv, lr, agg));
     }
     if (!more) break;
+    t = tn;
     T = Tn;
     wv = nwv;
 #pragma unroll
