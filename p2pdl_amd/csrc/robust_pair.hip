@@ -149,15 +149,30 @@ __device__ __forceinline__ void pin(const T (&x)[kHalf]) {
 // One half sorted in T's domain (the block's: keys if either half holds a
 // NaN); returns the aggregate, valid where `own`.  Both waves pass the same
 // number of block barriers.
-template <int RULE, typename T>
-__device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, int h, int lane) {
+template <int RULE>
+__device__ __attribute__((noinline)) float pair_keys(const float* const* P, int64_t c0, uint32_t lane_off, Img im,
+                                                     int h, int lane);
+
+// FLAGS (float path): the two waves swap "my half holds a NaN" at barrier 1,
+// beside the hand-off; a block that finds one re-runs the tile on the key
+// network (pair_keys) -- the float sort of a NaN half is discarded.
+template <int RULE, typename T, bool FLAGS = false>
+__device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, int h, int lane,
+                                           int __attribute__((address_space(3)))* flags = nullptr, bool nan = false,
+                                           const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0) {
   T x[kHalf];
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) x[j] = from_bits<T>(v[j]);
   sort_full<kHalf>(x);
   pin(x);
   if (h == 0) store_half(im, x, lane);
+  if constexpr (FLAGS) {
+    if (lane == 0) flags[h] = nan ? 1 : 0;
+  }
   block_sync();  // 1: A in the image
+  if constexpr (FLAGS) {
+    if (uniform((flags[0] | flags[1]) != 0)) return pair_keys<RULE>(P, c0, lane_off, im, h, lane);
+  }
   if constexpr (RULE == P2P_RULE_MEDIAN) {
     return h == 1 ? median_final(im, x, lane) : 0.f;
   } else {
@@ -241,12 +256,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
   const uint32_t lane_off = static_cast<uint32_t>((i < N ? i : N - 1) - c0) * 4u;
   uint32_t v[kHalf];
   load_half(v, P, c0, lane_off, h);
-  // One domain per block: the float network unless either half holds a NaN.
+  // One domain per block: the float network unless either half holds a NaN
+  // (flags swapped at the hand-off barrier, no barrier of their own).
   const bool nan = uniform(wave_has_nan(v));
-  if (lane == 0) nan_flag[h] = nan ? 1 : 0;
-  block_sync();
-  const bool keys = uniform((nan_flag[0] | nan_flag[1]) != 0);
-  const float agg = keys ? pair_keys<RULE>(P, c0, lane_off, im, h, lane) : pair_body<RULE, fk>(v, im, h, lane);
+  const float agg = pair_body<RULE, fk, true>(v, im, h, lane, (int __attribute__((address_space(3)))*)nan_flag, nan,
+                                              P, c0, lane_off);
   const bool own = RULE == P2P_RULE_MEDIAN ? h == 1 : h == 0;
   if (own && i < N) {
     if (O) stg(O + i, agg);
