@@ -178,14 +178,15 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   } else {
     constexpr int b = (2 * kHalf * 2) / 10;  // 51
     constexpr int hi = 2 * kHalf - b;        // 205: ranks b..hi-1 kept
-    auto part = (float __attribute__((address_space(3)))*)im;
+    // the partial sum has a slot of its own past the image (no barrier
+    // between wave 0's reads of U and wave 1's write of the partial)
+    auto part = (float __attribute__((address_space(3)))*)(im + kHalf / 4 * 64);
     if (h == 1) {
       flip_write_upper(im, x, lane);
       block_sync();  // 2: U_j in A_{127-j}'s word
       net_bmerge128_r51_127<true>(x);
-      block_sync();  // 3: wave 0 has read U
       part[lane] = sum_ranks<b, kHalf>(x, 0.f);
-      block_sync();  // 4: the partial sum of ranks 51..127 in the image
+      block_sync();  // 3: the partial sum of ranks 51..127 in its slot
       return 0.f;
     }
     block_sync();  // 2
@@ -193,7 +194,6 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
     for (int j = 0; j < kHalf; ++j) x[j] = from_raw<T>(img_at(im, kHalf - 1 - j, lane));
     net_bmerge128_r0_76<true>(x);
     block_sync();  // 3
-    block_sync();  // 4
     return sum_ranks<0, hi - kHalf>(x, part[lane]) / static_cast<float>(hi - b);
   }
 }
@@ -233,7 +233,7 @@ template <int RULE, bool SEGS>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(const float* const* __restrict__ peers,
                                                           const Seg* __restrict__ segs, int nseg, int64_t n,
                                                           float* w, float* out, float lr) {
-  __shared__ u32x4 img_raw[kHalf / 4 * 64];  // 32 KB
+  __shared__ u32x4 img_raw[kHalf / 4 * 64 + 16];  // 32 KB image + the trimmed mean's partial sums (256 B)
   __shared__ int nan_flag[2];
   Img im = (Img)img_raw;
   const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
