@@ -102,6 +102,26 @@ __device__ __forceinline__ float median_final(Img im, const T (&b)[kHalf], int l
   return val(m);
 }
 
+// median, split: this wave's sorted half X (registers) against the other
+// wave's half Y, of which the image holds groups 16..31 (elements 64..127):
+// max over X's groups 0..15 of min(X_j, Y_{127-j}).  Wave 1 (X = B) covers
+// j = 0..63, wave 0 (X = A, Y = B) covers the symmetric pairs (A_i, B_{127-i})
+// for i = 0..63, i.e. j = 64..127 -- together every L_j once.
+template <typename T>
+__device__ __forceinline__ T median_half(Img im, const T (&x)[kHalf], int lane) {
+  T m{};
+#pragma unroll
+  for (int g = 0; g < kHalf / 8; ++g) {
+    const u32x4 y4 = im[(kHalf / 8 - 1 - g) * 64 + lane];  // Y_{127-4g-k} = word 3-k of slot 15-g
+    const T l0 = min(x[4 * g], from_raw<T>(y4[3])), l1 = min(x[4 * g + 1], from_raw<T>(y4[2]));
+    const T l2 = min(x[4 * g + 2], from_raw<T>(y4[1])), l3 = min(x[4 * g + 3], from_raw<T>(y4[0]));
+    const T q = max(max(l0, l1), max(l2, l3));
+    m = g == 0 ? q : max(m, q);
+    if (g % kReadAhead == kReadAhead - 1) fence_after(m);
+  }
+  return m;
+}
+
 // trimmed, wave 1: L_j = min(B_j, A_{127-j}) stays in b; U_j = max(...) is
 // written over A_{127-j}'s word (each slot is read before it is rewritten).
 template <typename T>
@@ -165,7 +185,16 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   for (int j = 0; j < kHalf; ++j) x[j] = from_bits<T>(v[j]);
   sort_full<kHalf>(x);
   pin(x);
-  if (h == 0) store_half(im, x, lane);
+  if constexpr (RULE == P2P_RULE_MEDIAN) {
+    // each wave hands over its upper 64 (groups 16..31) into its own half of the image
+    Img mine = im + (h == 0 ? 0 : kHalf / 8 * 64);
+#pragma unroll
+    for (int g = kHalf / 8; g < kHalf / 4; ++g)
+      mine[(g - kHalf / 8) * 64 + lane] =
+          u32x4{raw(x[4 * g]), raw(x[4 * g + 1]), raw(x[4 * g + 2]), raw(x[4 * g + 3])};
+  } else {
+    if (h == 0) store_half(im, x, lane);
+  }
   if constexpr (FLAGS) {
     if (lane == 0) flags[h] = nan ? 1 : 0;
   }
@@ -174,7 +203,12 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
     if (uniform((flags[0] | flags[1]) != 0)) return pair_keys<RULE>(P, c0, lane_off, im, h, lane);
   }
   if constexpr (RULE == P2P_RULE_MEDIAN) {
-    return h == 1 ? median_final(im, x, lane) : 0.f;
+    // wave 1 pairs its B with A's upper half, wave 0 its A with B's upper half
+    auto part = (float __attribute__((address_space(3)))*)(im + kHalf / 4 * 64);
+    const T m = median_half(im + (h == 0 ? kHalf / 8 * 64 : 0), x, lane);
+    if (h == 0) part[lane] = __uint_as_float(raw(m));
+    block_sync();  // 2: wave 0's partial max in its slot
+    return h == 1 ? val(max(m, from_raw<T>(__float_as_uint(part[lane])))) : 0.f;
   } else {
     constexpr int b = (2 * kHalf * 2) / 10;  // 51
     constexpr int hi = 2 * kHalf - b;        // 205: ranks b..hi-1 kept
