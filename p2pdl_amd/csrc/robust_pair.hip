@@ -122,6 +122,27 @@ __device__ __forceinline__ T median_half(Img im, const T (&x)[kHalf], int lane) 
   return m;
 }
 
+// trimmed, split flip: this wave's half X against the other's upper half Y
+// (in `other`): for i < 64, lo/hi of (X_i, Y_{127-i}); KEEP_LO keeps lo at
+// X_i and parks hi at X_{64+i} (the upper half, already handed over), else
+// the reverse.
+template <bool KEEP_LO, typename T>
+__device__ __forceinline__ void flip_half(Img other, T (&x)[kHalf], int lane) {
+  constexpr int Q = kHalf / 2;
+#pragma unroll
+  for (int g = 0; g < Q / 4; ++g) {
+    const u32x4 y4 = other[(Q / 4 - 1 - g) * 64 + lane];  // Y_{127-4g-k} = word 3-k
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const T y = from_raw<T>(y4[3 - k]);
+      const T lo = min(x[4 * g + k], y), hi = max(x[4 * g + k], y);
+      x[4 * g + k] = KEEP_LO ? lo : hi;
+      x[Q + 4 * g + k] = KEEP_LO ? hi : lo;
+    }
+    if (g % kReadAhead == kReadAhead - 1) fence_after(x[4 * g + 3]);
+  }
+}
+
 // trimmed, wave 1: L_j = min(B_j, A_{127-j}) stays in b; U_j = max(...) is
 // written over A_{127-j}'s word (each slot is read before it is rewritten).
 template <typename T>
@@ -185,15 +206,14 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   for (int j = 0; j < kHalf; ++j) x[j] = from_bits<T>(v[j]);
   sort_full<kHalf>(x);
   pin(x);
-  if constexpr (RULE == P2P_RULE_MEDIAN) {
-    // each wave hands over its upper 64 (groups 16..31) into its own half of the image
+  {
+    // each wave hands over its upper 64 (groups 16..31) into its own half of
+    // the image: region R0 = A's (wave 0), R1 = B's (wave 1)
     Img mine = im + (h == 0 ? 0 : kHalf / 8 * 64);
 #pragma unroll
     for (int g = kHalf / 8; g < kHalf / 4; ++g)
       mine[(g - kHalf / 8) * 64 + lane] =
           u32x4{raw(x[4 * g]), raw(x[4 * g + 1]), raw(x[4 * g + 2]), raw(x[4 * g + 3])};
-  } else {
-    if (h == 0) store_half(im, x, lane);
   }
   if constexpr (FLAGS) {
     if (lane == 0) flags[h] = nan ? 1 : 0;
@@ -212,23 +232,38 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   } else {
     constexpr int b = (2 * kHalf * 2) / 10;  // 51
     constexpr int hi = 2 * kHalf - b;        // 205: ranks b..hi-1 kept
-    // the partial sum has a slot of its own past the image (no barrier
-    // between wave 0's reads of U and wave 1's write of the partial)
+    constexpr int Q = kHalf / 2;             // 64
     auto part = (float __attribute__((address_space(3)))*)(im + kHalf / 4 * 64);
-    if (h == 1) {
-      flip_write_upper(im, x, lane);
-      block_sync();  // 2: U_j in A_{127-j}'s word
+    // The flip split like the median: wave 1 takes the pairs (B_j, A_{127-j})
+    // for j < 64 (A's upper half from R0), wave 0 the pairs (A_i, B_{127-i})
+    // for i < 64 (B's upper half from R1), i.e. j = 127 - i >= 64.  Wave 1
+    // keeps L and sends its U_0..63 through R0; wave 0 keeps U and sends its
+    // L_64..127 through R1 (each wave rewrites only the region it read).
+    Img other = im + (h == 0 ? kHalf / 8 * 64 : 0);
+    if (h == 1) flip_half<true>(other, x, lane);  // wave 1: L_j at x[j], U_j parked at x[64 + j]
+    else flip_half<false>(other, x, lane);        // wave 0: U_{127-i} at x[i], L_{127-i} parked at x[64 + i]
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the region is read before it is rewritten
+#pragma unroll
+    for (int g = 0; g < Q / 4; ++g)  // wave 1: U_j (j < 64) in slot g; wave 0: L_{127-i} (i < 64) in slot g
+      other[g * 64 + lane] = u32x4{raw(x[Q + 4 * g]), raw(x[Q + 4 * g + 1]), raw(x[Q + 4 * g + 2]), raw(x[Q + 4 * g + 3])};
+    block_sync();  // 2: both parts handed over
+    if (h == 1) {  // L_64..127 = wave 0's L_{127-i}, i = 127 - j, from R1
+      Img r1 = im + kHalf / 8 * 64;
+#pragma unroll
+      for (int j = Q; j < kHalf; ++j) x[j] = from_raw<T>(img_at(r1, kHalf - 1 - j, lane));
       net_bmerge128_r51_127<true>(x);
       part[lane] = sum_ranks<b, kHalf>(x, 0.f);
       block_sync();  // 3: the partial sum of ranks 51..127 in its slot
       return 0.f;
     }
-    block_sync();  // 2
+    T u[kHalf];  // U_j: j < 64 from wave 1 through R0, j >= 64 kept at x[127 - j]
 #pragma unroll
-    for (int j = 0; j < kHalf; ++j) x[j] = from_raw<T>(img_at(im, kHalf - 1 - j, lane));
-    net_bmerge128_r0_76<true>(x);
+    for (int j = 0; j < Q; ++j) u[j] = from_raw<T>(img_at(im, j, lane));
+#pragma unroll
+    for (int j = Q; j < kHalf; ++j) u[j] = x[kHalf - 1 - j];
+    net_bmerge128_r0_76<true>(u);
     block_sync();  // 3
-    return sum_ranks<0, hi - kHalf>(x, part[lane]) / static_cast<float>(hi - b);
+    return sum_ranks<0, hi - kHalf>(u, part[lane]) / static_cast<float>(hi - b);
   }
 }
 
