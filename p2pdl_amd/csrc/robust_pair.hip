@@ -9,30 +9,33 @@
 // Wave h loads peers 128h..128h+127 of its 64 coordinates (every load
 // instruction reads 256 contiguous bytes of one peer) and sorts them in
 // VGPRs with Batcher's 128-key network -- half A (h = 0) and half B (h = 1).
-// Wave 0 hands its sorted A to wave 1 through LDS (32 KB: four keys per lane
-// per ds_write_b128), and the two sorted halves meet in one flip:
+// The two sorted halves meet in one flip:
 //   L_j = min(B_j, A_{127-j}),  U_j = max(B_j, A_{127-j})   (j = 0..127)
 // L is the 128 smallest keys of the coordinate, U the 128 largest, each a
-// bitonic sequence.
-//   median : rank 127 = max_j L_j -- wave 1 finishes with 128 v_min and 64
-//            v_max3, no merge at all.
-//   trimmed: wave 1 writes U back over A in LDS; wave 1 merges L pruned to
-//            ranks 51..127, wave 0 merges U pruned to ranks 0..76, and the
-//            ascending sum runs over L's ranks in wave 1 and carries on over
-//            U's in wave 0 (the partial sum crosses through LDS).
+// bitonic sequence.  Each wave hands its upper 64 keys to the other through
+// LDS (16 KB each, one ds_write_b128 per 4 keys) and takes half of the pairs:
+// wave 1 (B_j, A_{127-j}) for j < 64, wave 0 (A_i, B_{127-i}) for i < 64.
+//   median : rank 127 = max_j L_j -- each wave a partial max over its 64
+//            pairs (64 v_min, 32 v_max3), wave 0's crosses LDS; no merge.
+//   trimmed: wave 1 keeps L, wave 0 keeps U, the missing quarters cross LDS;
+//            wave 1 merges L pruned to ranks 51..127, wave 0 merges U pruned
+//            to ranks 0..76, and the ascending sum runs over L's ranks in
+//            wave 1 and carries on over U's in wave 0 (the partial crosses
+//            LDS through a slot of its own).
 // Against the 4-lanes-per-coordinate LDS kernel this issues ~10% (median) /
 // ~22% (trimmed) fewer VALU instructions per coordinate -- two 128-key sorts
 // instead of four 64-key sorts plus cross-lane bitonic merges, no DPP moves,
 // and the trimmed sum advances 64 coordinates per instruction instead of 16 --
-// and no wave only loads: every wave sorts, 2 per SIMD (≤ 256 VGPRs; 32 KB of
+// and no wave only loads: every wave sorts, 2 per SIMD (<= 256 VGPRs; 32 KB of
 // LDS per block, 4 blocks per CU), each hiding the other's HBM latency.
 //
-// Float or key network, per block: the two waves swap a "my half holds a
-// NaN" flag through LDS; without one the block sorts the float values
-// themselves (robust_nets.h: same order, same bits as the uint32 keys),
-// otherwise uint32 total-order keys.  The key path is out of line and
-// re-loads its inputs (pair_keys): inlined next to the float path, LLVM kept
-// both paths' 128 values live and the kernel took 320-390 VGPRs.
+// Float or key network, per block: each wave sorts its half on the float
+// values themselves (robust_nets.h: same order, same bits as the uint32
+// keys), and the two swap a "my half holds a NaN" flag at the hand-off
+// barrier; a block that finds one re-runs the tile on uint32 total-order
+// keys.  That key path is out of line and re-loads its inputs (pair_keys):
+// inlined next to the float path, LLVM kept both paths' 128 values live and
+// the kernel took 320-390 VGPRs.
 #include "robust_nets.h"
 
 namespace p2p {
