@@ -301,7 +301,10 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
   return pair_body<RULE, uint32_t>(v, im, h, lane);
 }
 
-template <int RULE, bool SEGS>
+// SMALL (flat buffers below 2^30 floats): the tile start rides in the 32-bit
+// lane offset and each peer row's pointer is the scalar base as loaded -- no
+// 64-bit scalar add per load (256 SALU instructions per wave and tile).
+template <int RULE, bool SEGS, bool SMALL = false>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(const float* const* __restrict__ peers,
                                                           const Seg* __restrict__ segs, int nseg, int64_t n,
                                                           float* w, float* out, float lr) {
@@ -325,14 +328,15 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
   }
   const int64_t i = c0 + lane;
   // Dead lanes of a ragged tail re-read the last element.
-  const uint32_t lane_off = static_cast<uint32_t>((i < N ? i : N - 1) - c0) * 4u;
+  const int64_t cb = SMALL ? 0 : c0;  // row base offset (0: the whole offset rides per lane)
+  const uint32_t lane_off = static_cast<uint32_t>((i < N ? i : N - 1) - cb) * 4u;
   uint32_t v[kHalf];
-  load_half(v, P, c0, lane_off, h);
+  load_half(v, P, cb, lane_off, h);
   // One domain per block: the float network unless either half holds a NaN
   // (flags swapped at the hand-off barrier, no barrier of their own).
   const bool nan = uniform(wave_has_nan(v));
   const float agg = pair_body<RULE, fk, true>(v, im, h, lane, (int __attribute__((address_space(3)))*)nan_flag, nan,
-                                              P, c0, lane_off);
+                                              P, cb, lane_off);
   const bool own = RULE == P2P_RULE_MEDIAN ? h == 1 : h == 0;
   if (own && i < N) {
     if (O) stg(O + i, agg);
@@ -355,9 +359,11 @@ extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, c
   const dim3 g(static_cast<unsigned>(grid)), b(2 * 64);
   if (rule == P2P_RULE_MEDIAN) {
     if (segs) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, false, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
     else hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
   } else {
     if (segs) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, false, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
     else hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
   }
 }
