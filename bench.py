@@ -85,7 +85,7 @@ WORKLOADS = {
     # params each) in the device slab vs the reference's pickle.loads
     "inbox": ("inbox", 16, 11_689_512, 0x5EED0007),
 }
-SUB_N1 = ["cfg2-dropin", "cfg4-median", "cfg4-trimmed", "median256", "trimmed256", "cfg5", "delta", "inbox"]
+SUB_N1 = ["cfg1", "cfg2-dropin", "cfg4-median", "cfg4-trimmed", "median256", "trimmed256", "cfg5", "delta", "inbox"]
 SUB_STEPS = {"cfg5": 2, "delta": 10, "inbox": 3}  # timed steps of the one-GPU sub-records
 MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
@@ -530,6 +530,9 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
         cpu = cpu_record(res, "GB/s", "port", f"{len(sizes)}-tensor state_dict ({n:,} params) x {K} updates, "
                                               f"reference per-key op sequence (aggregation.py:15-38) on torch "
                                               f"CPU, {res['reps']} reps in {res['seconds']}s")
+        # the same calls as microseconds per aggregate_models call (cfg1 is latency-bound)
+        cpu["us_per_call"] = round(4.0 * K * n / (res["value"] * 1e9) * 1e6, 1)
+        cpu["us_per_call_1thread"] = round(4.0 * K * n / (res["value_1thread"] * 1e9) * 1e6, 1)
     return {
         "workload": name.replace("-", "_"), "value": round(K * n * 4 / step_s / 1e9, 2), "unit": "GB/s",
         "ms_per_step": round(step_s * 1e3, 4), "us_per_call": round(step_s * 1e6, 1),
@@ -826,6 +829,37 @@ def replica_workload(args, name, dev):
 
 
 # ------------------------------------------------------------------ main
+SUB_KEEP = ("us_per_call", "us_per_call_general_path", "ms_per_job", "kernel_ms_sum", "allgather_ms_sum")
+ROOF_KEEP = ("kernel_ms", "vs_flat_kernel", "fedavg_ms", "chain_issue_bound_gbs")
+
+
+def compact_sub(rec: dict) -> dict:
+    """A sub-record as printed on the driver's line: the numbers only (the
+    workload definitions are WORKLOADS / the docstring above), so the whole
+    line -- cfg3_full included -- fits the driver's stdout tail."""
+    out = {"value": rec["value"], "unit": rec["unit"]}
+    if "ms_per_step" in rec:
+        out["ms"] = rec["ms_per_step"]
+    out.update({k: rec[k] for k in SUB_KEEP if k in rec})
+    roof = rec.get("roofline") or {}
+    if roof:
+        out["frac"] = roof.get("frac")
+        out.update({k: roof[k] for k in ROOF_KEEP if k in roof})
+        alg, tr = roof.get("alg_bytes_per_launch"), roof.get("traffic")
+        if alg and tr:
+            out["traffic_x"] = round(tr / alg, 5)
+    cfg = rec.get("config") or {}
+    for k in ("reference_ms", "with_digest"):
+        if k in cfg:
+            v = cfg[k]
+            out[k] = {a: b for a, b in v.items() if a != "what"} if isinstance(v, dict) else v
+    cpu = rec.get("cpu_baseline")
+    if cpu:
+        out["cpu"] = {k: cpu[k] for k in ("value", "unit", "cores", "value_1thread", "us_per_call", "kind")
+                      if k in cpu}
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -905,7 +939,7 @@ def main():
             "cpu_baseline": main_rec.get("cpu_baseline"),
         }
         if sub:
-            line["sub"] = sub
+            line["sub"] = {k: compact_sub(v) for k, v in sub.items()}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -31,7 +31,9 @@
 extern "C" {
 #endif
 
-#define P2P_ABI_VERSION 1
+/* 2: p2p_set_robust_layout (a process-global A/B switch of version 1) is
+ *    gone; every other entry point is unchanged. */
+#define P2P_ABI_VERSION 2
 
 typedef void *p2p_stream_t; /* hipStream_t */
 
@@ -81,9 +83,12 @@ int32_t p2p_fedavg_apply_devk_f32(const float *const *peers, const int32_t *k_de
 /* ---- K2: robust rules (build-defined: reference README.md:10 TODO) -----
  * median: rank (K-1)/2 under the IEEE total order on float bits.
  * trimmed: ascending fp32 sum of sorted ranks b..K-b-1 from +0, / (K-2b).
- * k <= 256.  Kernel family (fixed per k, no process state): one lane per
- * coordinate for k <= 128; 4 lanes x 64 keys, peer rows LDS-DMA staged, for
- * k in 129..256. */
+ * k <= 256.  Kernel family (a pure function of (rule, k, trim_b); no process
+ * state): one lane per coordinate for k <= 128; for k = 256 with the median
+ * or the default trim (b = 51) one lane per coordinate in two-wave blocks,
+ * each wave holding 128 peers (robust_pair.hip); for every other k in
+ * 129..256 (or trim) 4 lanes x 64 keys per coordinate, peer rows LDS-DMA
+ * staged (robust_lds.hip). */
 int32_t p2p_median_f32(const float *const *peers, int32_t k, int64_t n, float *out,
                        p2p_stream_t stream);
 int32_t p2p_trimmed_mean_f32(const float *const *peers, int32_t k, int64_t n, int32_t trim_b,

@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # P2P_LIB selects a diagnostic build (csrc/Makefile `diag`); default: the product library
 LIB_PATH = os.environ.get("P2P_LIB") or os.path.join(_HERE, "libp2pdl_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2  # include/p2pdl.h P2P_ABI_VERSION
 
 P2P_RULE_FEDAVG, P2P_RULE_MEDIAN, P2P_RULE_TRIMMED = 0, 1, 2
 

@@ -150,6 +150,7 @@ def _slab_fast_path(state, keys, received, rule, lr, trim_frac) -> bool:
             return False
         ws.append(t)
         offsets.append(off)
+    inbox.order_after_landing()  # land()'s row copies ran on the listener thread's stream
     ops.aggregate_slab_rows_(ws, inbox.slab, [rm["model"].row for rm in received], offsets, rule,
                              lr=lr, trim_frac=trim_frac)
     return True

@@ -26,7 +26,47 @@ namespace p2p {
 
 constexpr int kRobustTile = 128;  // coordinates per block (one lane each)
 
+// K == KP, no NaN in the wave: the pruned rules on the float values (robust_nets.h:
+// same ranks and bits as the keys) -- no key map in (2 VALU per key) or out.
+template <int KP, int RULE>
+__device__ __forceinline__ float special_floats(const uint32_t (&v)[KP]) {
+  if constexpr (RULE == P2P_RULE_MEDIAN) {
+    constexpr int Q = KP / 4;
+    fk a[Q], b[Q], c[Q], d[Q];
+#pragma unroll
+    for (int j = 0; j < Q; ++j) {
+      a[j].x = __uint_as_float(v[j]);
+      b[j].x = __uint_as_float(v[Q + j]);
+      c[j].x = __uint_as_float(v[2 * Q + j]);
+      d[j].x = __uint_as_float(v[3 * Q + j]);
+    }
+    sort_full<Q>(a);
+    sort_full<Q>(b);
+    sort_full<Q>(c);
+    sort_full<Q>(d);
+    return four_list_median<Q>(a, b, c, d).x;
+  } else {
+    fx x[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) x[j].x = __uint_as_float(v[j]);
+    run_special<KP, 2>(x);
+    constexpr int b = (KP * 2) / 10;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = b; j < KP - b; ++j) acc = __fadd_rn(acc, x[j].x);
+    return acc / static_cast<float>(KP - 2 * b);
+  }
+}
+
 template <int KP, int RULE, int MODE>
+__device__ __attribute__((noinline)) float robust_coord_keys(const float* const* peers, int K, int trim_b,
+                                                             int64_t c0, uint32_t lane_off);
+
+// KEYS: the uint32 total-order key network (MODE 0, or a wave holding a NaN);
+// otherwise (K == KP) the float network unless the wave holds a NaN, which
+// re-runs on the keys out of line (re-loading: inlined, LLVM kept both
+// paths' values live, 256 VGPRs and one wave per SIMD).
+template <int KP, int RULE, int MODE, bool KEYS = MODE == 0>
 __device__ __forceinline__ float robust_coord(const float* const* __restrict__ peers, int K,
                                               int trim_b, int64_t c0, uint32_t lane_off) {
   // Loads are unconditional (a pad slot re-reads peer 0, an L2 hit) so the
@@ -45,12 +85,34 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
         reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off)));
   }
   __builtin_amdgcn_sched_barrier(0);  // all KP loads in flight before the first use
+  if constexpr (MODE != 0 && !KEYS) {  // K == KP: a NaN-free wave runs on the floats themselves
+    if (!__builtin_amdgcn_readfirstlane(static_cast<int>(wave_has_nan(v)))) return special_floats<KP, RULE>(v);
+    return robust_coord_keys<KP, RULE, MODE>(peers, K, trim_b, c0, lane_off);
+  }
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
     const bool real = (MODE != 0) || (j < K);
     v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pad: sorts after every real key
   }
-  if constexpr (MODE == 0) {
+  if constexpr (RULE == P2P_RULE_MEDIAN && MODE == 1) {
+    // K == KP in {64, 128}: four sorted lists of KP/4 and the two-set search
+    // (robust_nets.h) -- 1.9k VALU at K = 128 against 2.3k for the pruned
+    // Batcher median network.
+    constexpr int Q = KP / 4;
+    uint32_t a[Q], b[Q], c[Q], d[Q];
+#pragma unroll
+    for (int j = 0; j < Q; ++j) {
+      a[j] = v[j];
+      b[j] = v[Q + j];
+      c[j] = v[2 * Q + j];
+      d[j] = v[3 * Q + j];
+    }
+    sort_full<Q>(a);
+    sort_full<Q>(b);
+    sort_full<Q>(c);
+    sort_full<Q>(d);
+    return __uint_as_float(key2f(four_list_median<Q>(a, b, c, d)));
+  } else if constexpr (MODE == 0) {
     sort_full<KP>(v);
   } else if constexpr (RULE == P2P_RULE_TRIMMED && KP == 128) {  // fewer live VGPRs: 3 waves/SIMD
     kx x[KP];
@@ -92,6 +154,17 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
   }
 }
 
+template <int KP, int RULE, int MODE>
+__device__ __attribute__((noinline)) float robust_coord_keys(const float* const* peers, int K, int trim_b,
+                                                             int64_t c0, uint32_t lane_off) {
+  // arguments arrive in VGPRs: make the wave-uniform ones scalar again
+  peers = reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(peers)));
+  c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(c0)));
+  K = __builtin_amdgcn_readfirstlane(K);
+  trim_b = __builtin_amdgcn_readfirstlane(trim_b);
+  return robust_coord<KP, RULE, MODE, true>(peers, K, trim_b, c0, lane_off);
+}
+
 // ---- kernels ---------------------------------------------------------------
 // KP <= 128 (template arg): one lane per coordinate, 128-lane blocks.
 // P in {2, 4} (GROUP kernels): 128*P-lane blocks.  A block covers kRobustTile
@@ -108,14 +181,14 @@ __device__ __forceinline__ void robust_one(const float* const* peers, int K, int
 }
 
 template <int KP, int RULE, int MODE>
-__global__ __launch_bounds__(kRobustTile) void robust_flat_kernel(
+__global__ __launch_bounds__(kRobustTile, MODE != 0 ? 3 : 1) void robust_flat_kernel(
     const float* const* __restrict__ peers, int K, int trim_b, int64_t n, float* w, float* out,
     float lr) {
   robust_one<KP, RULE, MODE>(peers, K, trim_b, n, bid_x(), w, out, lr);
 }
 
 template <int KP, int RULE, int MODE>
-__global__ __launch_bounds__(kRobustTile) void robust_segments_kernel(
+__global__ __launch_bounds__(kRobustTile, MODE != 0 ? 3 : 1) void robust_segments_kernel(
     const Seg* __restrict__ segs, int nseg, int K, int trim_b, float lr) {
   const int64_t t = bid_x();
   const Seg s = load_segment(segs, nseg, t);

@@ -36,39 +36,12 @@
 // Tiles that cannot be DMA'd (a peer / w pointer not 16-B aligned, or the
 // ragged last tile of a buffer) load the same keys with per-lane global
 // loads; the arithmetic after the load is the same code.
-// Packed 16-bit keys (two coordinates per VGPR, radix16 layout): declared
-// before the networks so their unqualified min / max calls resolve for u16x2.
-#include <hip/hip_runtime.h>
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ u16x2 min(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
-__device__ __forceinline__ u16x2 max(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
-__device__ __forceinline__ u16x2 pmin(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
-__device__ __forceinline__ u16x2 pmax(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
-
 #include "robust_nets.h"
 
 #define P2P_LDS __attribute__((address_space(3)))
 
-// Diagnostic builds only (make diag): 1 = no DMA (sort stale LDS: compute
-// time), 2 = no sort (DMA + barriers + stores: staging time), 3 = trimmed
-// mean without the rank-ordered sum (sort + staging).  Wrong results.
-#ifndef P2P_LDS_DIAG
-#define P2P_LDS_DIAG 0
-#endif
-// A/B build only (make nofloat): the uint32-key network for every wave.
-#ifndef P2P_NO_FLOAT_PATH
-#define P2P_NO_FLOAT_PATH 0
-#endif
-// A/B build only (make nopair): K = 256 on the 4-lane kernel, not robust_pair.hip.
-#ifndef P2P_NO_PAIR
-#define P2P_NO_PAIR 0
-#endif
-
 namespace p2p {
 
-__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
-  return max(min(a, b), min(max(a, b), c));  // -> v_med3_u32
-}
 
 // DPP move with bound_ctrl: every lane is written, so no "old" operand has to
 // be materialised (update_dpp(0, ...) cost a v_mov_b32 per exchange).
@@ -88,13 +61,8 @@ __device__ __forceinline__ fk xq(fk x) {
 }
 
 // Type-generic pieces of the L-lane reduction: uint32 total-order keys or
-// float values (NaN-free waves, robust_nets.h).  keep(a, p, hi) is
-// min(a, p) / max(a, p) in ONE v_med3 against a lane-constant 0 / ~0 (keys)
-// or -inf / +inf (floats); value() is the float the element stands for.
-__device__ __forceinline__ uint32_t keep(uint32_t a, uint32_t p, uint32_t lim) { return umed3(a, p, lim); }
-__device__ __forceinline__ fk keep(fk a, fk p, fk lim) { return fk{__builtin_amdgcn_fmed3f(a.x, p.x, lim.x)}; }
-__device__ __forceinline__ uint32_t keep_limit(uint32_t, bool hi) { return hi ? 0xFFFFFFFFu : 0u; }
-__device__ __forceinline__ fk keep_limit(fk, bool hi) { return fk{hi ? __builtin_inff() : -__builtin_inff()}; }
+// float values (NaN-free waves, robust_nets.h; keep / keep_limit there);
+// value() is the float the element stands for.
 __device__ __forceinline__ float value(uint32_t k) { return __uint_as_float(key2f(k)); }
 __device__ __forceinline__ float value(fk f) { return f.x; }
 
@@ -105,11 +73,11 @@ __device__ __forceinline__ float from_prev_slice(float x) {
   return __uint_as_float(dpp<L == 4 ? 0x90 : 0xA0>(__float_as_uint(x)));
 }
 
-template <int L, int H, int NB = 0, int PK = 1>
+template <int L, int H, int NB = 0>
 struct LdsLayout {
   static constexpr int W = 4;                  // sorter waves per block (and as many loaders)
-  static constexpr int TB = 64 * W * PK / L;   // coordinates per block tile
-  static constexpr int TW = 64 * PK / L;       // coordinates per sorter wave (PK per lane group)
+  static constexpr int TB = 64 * W / L;        // coordinates per block tile
+  static constexpr int TW = 64 / L;            // coordinates per sorter wave
   static constexpr int RB = 4 * TB;            // bytes per peer row (>= 256 contiguous in HBM)
   static constexpr int PAD = L > 1 ? 128 / L : 0;
   static constexpr int SB = H * RB + PAD;      // bytes per slice
@@ -226,13 +194,6 @@ __device__ __forceinline__ float reduce_keys(T (&v)[H], int q, int K, int trim_b
       own = (q == r / H);
       return value(sel);
     } else {
-      if constexpr (P2P_LDS_DIAG == 3) {  // diag: no sum (keep the sort live)
-        uint32_t x = __float_as_uint(value(v[0]));
-#pragma unroll
-        for (int j = 1; j < H; ++j) x ^= __float_as_uint(value(v[j]));
-        own = (q == L - 1);
-        return __uint_as_float(x);
-      }
       // ascending-rank sequential sum from +0: slice 0's ranks, then slice 1 ...
       constexpr int KP = L * H;
       const int b = MODE == 2 ? (KP * 2) / 10 : trim_b;
@@ -258,134 +219,15 @@ __device__ __forceinline__ float reduce_keys(T (&v)[H], int q, int K, int trim_b
   }
 }
 
-// ---- two-pass radix median, K = 256 (layout "radix16", PK = 2) -------------
-// Two coordinates per lane group: lane 4c+q holds keys 64q..64q+63 of
-// coordinates c (ka) and c+16 (kb).  Pass 1 runs the L = 4 median chain on
-// packed u16x2 keys -- a 16-bit image of both coordinates' keys in one VGPR --
-// because v_pk_min/max_u16 sort two keys per half-rate instruction.  The
-// 16-bit image is a per-coordinate AFFINE map of the uint32 key,
-//   k16 = sat16(sat_sub(key, base) >> s),
-// with base / s from the min / max of 32 sampled keys (8 per lane), so the
-// 65536 buckets span the data's actual range (round 1's hi16-of-the-raw-key
-// image put ~86% of waves on the fallback: the median's neighbours shared a
-// bucket).  The map is monotone (non-decreasing), so the rank-127 bucket mh
-// holds the median; pass 1 also yields the rank-126 bucket.  When rank 126's
-// bucket < mh, exactly 127 keys lie below mh's bucket and the median is the
-// SMALLEST key >= lo = base + (mh << s): one min over (key - lo) (keys below
-// lo wrap above every key >= lo).  Otherwise -- a tie across ranks 126/127,
-// or mh saturated at 0 / 65535 -- the wave runs the exact uint32 chain on
-// both coordinates.
-__device__ __forceinline__ uint32_t pbits(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
-__device__ __forceinline__ u16x2 pvec(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
-template <int M>
-__device__ __forceinline__ u16x2 pxq(u16x2 x) { return pvec(xq<M>(pbits(x))); }
-__device__ __forceinline__ u16x2 pkeep(u16x2 a, u16x2 pa, bool hi) {
-  const u16x2 lo = pmin(a, pa), h = pmax(a, pa);
-  return hi ? h : lo;
-}
-
-#ifdef P2P_LAB
-__device__ int g_lab_fallback[64];  // lab builds only: waves that took the exact fallback
-#endif
-
-// base / shift of the affine 16-bit map from the quad's 32 sampled keys
-// (this lane's keys 0..7): every key in [min, max] of the sample maps without
-// saturation, the rest saturates to 0 / 65535 (still monotone).
-__device__ __forceinline__ void affine_params(const uint32_t (&k)[64], uint32_t& base, uint32_t& s) {
-  uint32_t lo = k[0], hi = k[0];
-#pragma unroll
-  for (int j = 1; j < 8; ++j) {
-    lo = min(lo, k[j]);
-    hi = max(hi, k[j]);
-  }
-  lo = min(lo, xq<1>(lo));
-  hi = max(hi, xq<1>(hi));
-  lo = min(lo, xq<2>(lo));
-  hi = max(hi, xq<2>(hi));
-  const uint32_t range = hi - lo;
-  const uint32_t bits = range ? 32u - static_cast<uint32_t>(__builtin_clz(range)) : 0u;
-  base = lo;
-  s = bits > 16u ? bits - 16u : 0u;
-}
-
-__device__ __forceinline__ uint32_t affine16(uint32_t key, uint32_t base, uint32_t s) {
-  return __builtin_elementwise_sub_sat(key, base) >> s;  // saturated to 16 bits by the pack
-}
-
-__device__ __forceinline__ void radix_median_pair(uint32_t (&ka)[64], uint32_t (&kb)[64], int q, float& ra,
-                                                  float& rb) {
-  uint32_t base_a, s_a, base_b, s_b;
-  affine_params(ka, base_a, s_a);
-  affine_params(kb, base_b, s_b);
-  u16x2 h[64];
-#pragma unroll
-  for (int j = 0; j < 64; ++j)  // v_cvt_pk_u16_u32: two u32 -> u16x2, each saturated at 0xFFFF
-    h[j] = __builtin_amdgcn_cvt_pk_u16(static_cast<int>(affine16(ka[j], base_a, s_a)),
-                                       static_cast<int>(affine16(kb[j], base_b, s_b)));
-  sort_full<64>(h);  // the generated networks are type-generic (min / max below)
-  const bool k1 = q & 1, k2 = q & 2;
-#pragma unroll
-  for (int j = 0; j < 32; ++j) {  // flip against lane q^1
-    const u16x2 a = h[j], b = h[63 - j];
-    h[j] = pkeep(a, pxq<1>(b), k1);
-    h[63 - j] = pkeep(b, pxq<1>(a), k1);
-  }
-  bmerge<64>(h);
-#pragma unroll
-  for (int j = 0; j < 32; ++j) {  // flip against lane q^3
-    const u16x2 a = h[j], b = h[63 - j];
-    h[j] = pkeep(a, pxq<3>(b), k2);
-    h[63 - j] = pkeep(b, pxq<3>(a), k2);
-  }
-  // lanes q < 2 now hold the 128 smallest 16-bit keys of each coordinate:
-  // the largest two of them are ranks 127 and 126
-  u16x2 m1 = h[0], m2 = pvec(0u);
-#pragma unroll
-  for (int j = 1; j < 64; ++j) {
-    m2 = pmax(m2, pmin(m1, h[j]));
-    m1 = pmax(m1, h[j]);
-  }
-  {
-    const u16x2 p1 = pxq<1>(m1), p2 = pxq<1>(m2);
-    m2 = pmax(pmin(m1, p1), pmax(m2, p2));
-    m1 = pmax(m1, p1);
-  }
-  const uint32_t mh = dpp<0x00>(pbits(m1)), sh = dpp<0x00>(pbits(m2));  // lane 4c's values to its quad
-  const uint32_t mha = mh & 0xFFFFu, mhb = mh >> 16;
-  const bool fast = (sh & 0xFFFFu) < mha && (sh >> 16) < mhb && mha != 0xFFFFu && mhb != 0xFFFFu;
-  if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
-    const uint32_t la = base_a + (mha << s_a), lb = base_b + (mhb << s_b);  // smallest key of bucket mh
-    uint32_t ua = 0xFFFFFFFFu, ub = 0xFFFFFFFFu;
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      ua = min(ua, ka[j] - la);
-      ub = min(ub, kb[j] - lb);
-    }
-    ua = min(ua, xq<1>(ua));
-    ub = min(ub, xq<1>(ub));
-    ua = min(ua, xq<2>(ua));
-    ub = min(ub, xq<2>(ub));
-    ra = __uint_as_float(key2f(ua + la));
-    rb = __uint_as_float(key2f(ub + lb));
-  } else {  // valid in lane q == 0 either way
-#ifdef P2P_LAB
-    atomicAdd(&g_lab_fallback[tid_x() & 63], 1);  // per-lane slots: a vector atomic
-#endif
-    bool own = false;
-    ra = reduce_keys<4, 64, P2P_RULE_MEDIAN, 1>(ka, q, 256, 0, own);
-    rb = reduce_keys<4, 64, P2P_RULE_MEDIAN, 1>(kb, q, 256, 0, own);
-  }
-}
-
 // Register-staged fill of the LDS image for a tile that cannot be DMA'd
 // (misaligned pointer or ragged tail): each lane writes exactly the words it
 // reads back.  Out of line: its row-pointer loads must not share the
 // register budget of the sorting loop.
-template <int L, int H, int PK>
+template <int L, int H>
 __device__ __attribute__((noinline)) void fill_direct(uint8_t P2P_LDS* lds, const float* const* tbl,
                                                       const float* w, int64_t n, int64_t i, int K, int q,
                                                       int c) {
-  using Lay = LdsLayout<L, H, 0, PK>;
+  using Lay = LdsLayout<L, H>;
   const int64_t ic = i < n ? i : n - 1;  // dead lanes re-read the last element
   uint32_t P2P_LDS* sl = (uint32_t P2P_LDS*)(lds + q * Lay::SB) + c;
 #pragma unroll
@@ -433,14 +275,13 @@ __device__ __forceinline__ void block_sync_lds() {
 // next tile in flight while the sorters work on the current one.  Per tile:
 //   loaders: wait own pieces of tile t | barrier A | barrier B | DMA(t+2 grid)
 //   sorters: (fill if not DMA-able)   | barrier A | read      | barrier B | sort, store
-template <int L, int H, int RULE, int MODE, bool SEGS, int NB, int PK = 1>
+template <int L, int H, int RULE, int MODE, bool SEGS, int NB>
 __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __restrict__ peers,
                                                              const Seg* __restrict__ segs, int nseg,
                                                              int64_t ntiles, int K, int trim_b, int64_t n,
                                                              float* w, float* out, float lr, int64_t nb) {
-  using Lay = LdsLayout<L, H, NB, PK>;
+  using Lay = LdsLayout<L, H, NB>;
   static_assert(128 * Lay::W == 512, "launch bounds");
-  static_assert(PK == 1 || (L == 4 && H == 64 && RULE == P2P_RULE_MEDIAN && MODE == 1), "radix16: median of 256");
   __shared__ __attribute__((aligned(16))) uint8_t lds_raw[Lay::BYTES];
   uint8_t P2P_LDS* lds = (uint8_t P2P_LDS*)lds_raw;
   const int wi = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
@@ -459,7 +300,7 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
   // on a pointer load while the next tile's DMA is outstanding); with one
   // image they are reloaded per tile (L2 hits) so the sorters' 128 keys keep
   // the register file.
-  constexpr bool kCachePtr = Lay::NBUF == 2 || PK == 2;  // radix16: one image, VGPRs to spare
+  constexpr bool kCachePtr = Lay::NBUF == 2;
   const float* rp[kCachePtr ? Lay::NCHW : 1];
   int64_t cur_seg = -1;
   bool aligned = false;
@@ -491,7 +332,6 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
     return np + ((s.w && li == 0) ? 1 : 0);
   };
   auto issue = [&](const TileSrc& s, int img_off) {
-    if constexpr (P2P_LDS_DIAG == 1) return;
     uint8_t P2P_LDS* im = lds + img_off;
     const int64_t off = s.c0 + 4 * (lane % Lay::LPR);
 #pragma unroll
@@ -559,10 +399,7 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
     uint8_t P2P_LDS* im = lds + img;
     const TileSrc me = cur;
     const int64_t i = me.c0 + c;
-    if (!dma_cur) {
-      fill_direct<L, H, PK>(im, me.peers, me.w, me.n, i, K, q, c);
-      if constexpr (PK == 2) fill_direct<L, H, PK>(im, me.peers, me.w, me.n, i + 64 / L, K, q, c + 64 / L);
-    }
+    if (!dma_cur) fill_direct<L, H>(im, me.peers, me.w, me.n, i, K, q, c);
     __builtin_amdgcn_s_barrier();  // A: every piece of tile t is in the image
     asm volatile("" ::: "memory");
     uint32_t v[H];
@@ -570,70 +407,24 @@ __global__ __launch_bounds__(512) void robust_lds_kernel(const float* const* __r
 #pragma unroll
     for (int j = 0; j < H; ++j) v[j] = sl[j * (Lay::RB / 4)];
     const float wv = me.w ? ((const float P2P_LDS*)(im + Lay::WOFF))[c] : 0.f;
-    if constexpr (PK == 2) {  // radix16: the lane group's second coordinate, c + 16
-      constexpr int C2 = 64 / L;
-      uint32_t v2[H];
-#pragma unroll
-      for (int j = 0; j < H; ++j) v2[j] = sl[j * (Lay::RB / 4) + C2];
-      const float wv2 = me.w ? ((const float P2P_LDS*)(im + Lay::WOFF))[c + C2] : 0.f;
-      block_sync_lds();  // B
-      advance(t);
-#pragma unroll
-      for (int j = 0; j < H; ++j) {
-        v[j] = f2key(v[j]);
-        v2[j] = f2key(v2[j]);
-      }
-      float a1, a2;
-      if constexpr (P2P_LDS_DIAG == 2) {  // staging only
-        uint32_t x = 0, y = 0;
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-          x ^= v[j];
-          y ^= v2[j];
-        }
-        a1 = __uint_as_float(x);
-        a2 = __uint_as_float(y);
-      } else {
-        radix_median_pair(v, v2, q, a1, a2);
-      }
-      if (q == 0) {
-        if (i < me.n) {
-          if (me.out) stg(me.out + i, a1);
-          if (me.w) stg(me.w + i, apply_lr(wv, lr, a1));
-        }
-        if (i + C2 < me.n) {
-          if (me.out) stg(me.out + i + C2, a2);
-          if (me.w) stg(me.w + i + C2, apply_lr(wv2, lr, a2));
-        }
-      }
-      continue;
-    }
     block_sync_lds();  // B: image consumed, free for the DMA D tiles ahead
     advance(t);
     bool own = false;
     float agg;
-    if constexpr (P2P_LDS_DIAG == 2) {
-      uint32_t x = 0;
+    bool fast = false;  // every slot real (K == KP) and no NaN in the wave: the float network
+    if constexpr (MODE != 0) fast = !wave_has_nan(v);
+    if (fast) {
+      fk f[H];
 #pragma unroll
-      for (int j = 0; j < H; ++j) x ^= v[j];
-      agg = __uint_as_float(x);
-      own = q == 0;
+      for (int j = 0; j < H; ++j) f[j].x = __uint_as_float(v[j]);
+      agg = reduce_keys<L, H, RULE, MODE>(f, q, K, trim_b, own);
     } else {
-      bool fast = false;  // every slot real (K == KP) and no NaN in the wave: the float network
-      if constexpr (MODE != 0 && !P2P_NO_FLOAT_PATH) fast = !wave_has_nan(v);
-      if (fast) {
-        fk f[H];
 #pragma unroll
-        for (int j = 0; j < H; ++j) f[j].x = __uint_as_float(v[j]);
-        agg = reduce_keys<L, H, RULE, MODE>(f, q, K, trim_b, own);
-      } else {
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-          const bool real = (MODE != 0) || (q * H + j < K);
-          v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pads sort after every real key
-        }
-        agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
+      for (int j = 0; j < H; ++j) {
+        const bool real = (MODE != 0) || (q * H + j < K);
+        v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pads sort after every real key
       }
+      agg = reduce_keys<L, H, RULE, MODE>(v, q, K, trim_b, own);
     }
     if (own && i < me.n) {
       if (me.out) stg(me.out + i, agg);
@@ -736,7 +527,7 @@ __global__ __launch_bounds__(768) void robust_lds_g2_kernel(const float* const* 
     if (has) {
       me = locate<Lay::TB, SEGS>(peers, segs, nseg, n, w, out, tt);
       bind(me);
-      if (!dma_ok(me)) fill_direct<L, H, 1>(im, me.peers, me.w, me.n, me.c0 + c, K, q, c);
+      if (!dma_ok(me)) fill_direct<L, H>(im, me.peers, me.w, me.n, me.c0 + c, K, q, c);
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // A: both images hold their tiles
@@ -776,10 +567,10 @@ struct LdsArgs {
   hipStream_t stream;
 };
 
-template <int L, int H, int RULE, int MODE, bool SEGS, int NB, int PK = 1>
+template <int L, int H, int RULE, int MODE, bool SEGS, int NB>
 static void launch_lds_kernel(const LdsArgs& a) {
-  using Lay = LdsLayout<L, H, NB, PK>;
-  auto kern = robust_lds_kernel<L, H, RULE, MODE, SEGS, NB, PK>;
+  using Lay = LdsLayout<L, H, NB>;
+  auto kern = robust_lds_kernel<L, H, RULE, MODE, SEGS, NB>;
   constexpr int kThreads = 128 * Lay::W;
   static int resident = 0;  // persistent grid: every resident block slot once
   if (resident == 0) {
@@ -850,7 +641,7 @@ using namespace p2p;
 // K in 129..256: 4 lanes x 64 keys per coordinate, 64-coordinate tiles in
 // both block shapes (p2p_robust_lds_tile and the launch must agree; the tile
 // size is a pure function of (rule, k)).  Other
-// instantiations of the templates above (4 x 32, 2 x 64, 1 x 128, radix16)
+// instantiations of the templates above (4 x 32, 2 x 64, 1 x 128, 2 x 128)
 // are built only into the A/B library of tools/robust_lab.hip.
 extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t rule, int32_t k) {
   (void)rule;
@@ -863,8 +654,7 @@ extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, c
                                                     float* w, float* out, float lr, p2p_stream_t stream);
 
 // K = 256 with the default trim (the pruned networks): one lane per
-// coordinate in two-wave blocks, robust_pair.hip (A/B build P2P_NO_PAIR: the
-// 4-lane kernel above, one sorter group per block).  Any other K in 129..255 or trim runs the generic
+// coordinate in two-wave blocks, robust_pair.hip.  Any other K in 129..255 or trim runs the generic
 // padded network -- ~1.4x the instructions -- where two sorter groups per
 // block are faster (median -7%, trimmed -12% time for K in 129..255, round-2
 // lab A/B, profiles/r02/ab/labg2k); for the pruned K = 256 networks the
@@ -877,12 +667,7 @@ extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, co
   const bool med = rule == P2P_RULE_MEDIAN;
   const bool pruned = k == 256 && (med || trim_b == (256 * 2) / 10);
   if (pruned) {
-#if P2P_NO_PAIR
-    if (med) launch_lds_mode<4, 64, P2P_RULE_MEDIAN, 1, 0>(a);
-    else launch_lds_mode<4, 64, P2P_RULE_TRIMMED, 2, 0>(a);
-#else
     p2p_robust_pair_launch(peers, segs, nseg, tiles, rule, n, w, out, lr, stream);
-#endif
   } else if (med) {
     if (segs) launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, true>(a); else launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, false>(a);
   } else {

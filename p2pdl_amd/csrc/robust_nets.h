@@ -63,6 +63,20 @@ __device__ __forceinline__ void ce(kx& a, kx& b) {
   const uint32_t lo = ::min(a.k, b.k), hi = __builtin_amdgcn_bitop3_b32(a.k, b.k, lo, 0x96);
   if constexpr (ASC) { a.k = lo; b.k = hi; } else { a.k = hi; b.k = lo; }
 }
+// The same for NaN-free floats: v_min_f32 returns one of its inputs bit for
+// bit (-0 < +0), so the larger is again a ^ b ^ min(a, b).
+struct fx {
+  float x;
+};
+__device__ __forceinline__ fx min(fx a, fx b) { return fx{__builtin_fminf(a.x, b.x)}; }
+__device__ __forceinline__ fx max(fx a, fx b) { return fx{__builtin_fmaxf(a.x, b.x)}; }
+template <bool ASC>
+__device__ __forceinline__ void ce(fx& a, fx& b) {
+  const float lo = __builtin_fminf(a.x, b.x);
+  const float hi = __uint_as_float(
+      __builtin_amdgcn_bitop3_b32(__float_as_uint(a.x), __float_as_uint(b.x), __float_as_uint(lo), 0x96));
+  if constexpr (ASC) { a.x = lo; b.x = hi; } else { a.x = hi; b.x = lo; }
+}
 #define P2P_CE(a, b) ce<ASC>((a), (b))
 #define P2P_MIN(a, b) (a) = (ASC ? min((a), (b)) : max((a), (b)))
 #define P2P_MAX(a, b) (b) = (ASC ? max((a), (b)) : min((a), (b)))
@@ -70,6 +84,97 @@ __device__ __forceinline__ void ce(kx& a, kx& b) {
 #undef P2P_CE
 #undef P2P_MIN
 #undef P2P_MAX
+
+// keep(a, b, lim): min(a, b) when lim is the bottom of the order, max(a, b)
+// when it is the top -- ONE v_med3 against a lane-constant 0 / ~0 (keys) or
+// -inf / +inf (floats; v_med3_f32 orders -0 < +0, tools/fminmax_probe.hip).
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  return max(min(a, b), min(max(a, b), c));  // -> v_med3_u32
+}
+__device__ __forceinline__ uint32_t keep(uint32_t a, uint32_t p, uint32_t lim) { return umed3(a, p, lim); }
+__device__ __forceinline__ fk keep(fk a, fk p, fk lim) { return fk{__builtin_amdgcn_fmed3f(a.x, p.x, lim.x)}; }
+__device__ __forceinline__ uint32_t keep_limit(uint32_t, bool hi) { return hi ? 0xFFFFFFFFu : 0u; }
+__device__ __forceinline__ fk keep_limit(fk, bool hi) { return fk{hi ? __builtin_inff() : -__builtin_inff()}; }
+
+// a <= b in the total order.  Floats: min(a, b) is a bit for bit (an IEEE
+// compare calls -0 and +0 equal, and the two-set search below must not).
+__device__ __forceinline__ bool le(uint32_t a, uint32_t b) { return a <= b; }
+__device__ __forceinline__ bool le(fk a, fk b) {
+  return __float_as_uint(__builtin_fminf(a.x, b.x)) == __float_as_uint(a.x);
+}
+
+// max of N values as a tree of v_max3 (ceil((N-1)/2) instructions).
+template <int N, typename T>
+__device__ __forceinline__ T max_tree(const T* a) {
+  if constexpr (N == 1) return a[0];
+  else if constexpr (N == 2) return max(a[0], a[1]);
+  else if constexpr (N == 3) return max(max(a[0], a[1]), a[2]);
+  else {
+    constexpr int N1 = N / 3, N2 = (N - N1) / 2, N3 = N - N1 - N2;
+    return max(max(max_tree<N1>(a), max_tree<N2>(a + N1)), max_tree<N3>(a + N1 + N2));
+  }
+}
+
+// ---- median by a two-set search (no merge network) --------------------------
+// Lower median of X u Y for X, Y BITONIC of N keys each (rank N-1 of 2N).
+// Half-clean both: X_lo = min(X_i, X_{i+N/2}) holds the N/2 smallest of X,
+// X_hi the rest, each bitonic again.  If max(X_lo) <= max(Y_lo) (total order)
+// every key of X_lo ranks below the wanted one and every key of Y_hi above it,
+// so the answer is the lower median of X_hi u Y_lo; else of X_lo u Y_hi.
+// Ties choose either branch with the same value.  Per level: N/2 mins and a
+// max3 tree per set, one compare, then the kept halves as ONE v_med3 per key
+// against a lane-constant limit -- 2.5 VALU per key where a pruned merge
+// network pays 2 per comparator over log2 levels.  N = 1: min(X_0, Y_0).
+template <int N, typename T>
+__device__ __forceinline__ T two_set_median(const T (&x)[N], const T (&y)[N]) {
+  if constexpr (N == 1) {
+    return min(x[0], y[0]);
+  } else {
+    constexpr int H = N / 2;
+    T xl[H], yl[H];
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      xl[i] = min(x[i], x[i + H]);
+      yl[i] = min(y[i], y[i + H]);
+    }
+    const bool d = le(max_tree<H>(xl), max_tree<H>(yl));  // true: keep X_hi, Y_lo
+    const T lx = keep_limit(T{}, d), ly = keep_limit(T{}, !d);
+    T x2[H], y2[H];
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      x2[i] = keep(x[i], x[i + H], lx);
+      y2[i] = keep(y[i], y[i + H], ly);
+    }
+    return two_set_median<H>(x2, y2);
+  }
+}
+
+// Lower median of four SORTED lists p, q, r, s of N keys (rank 2N-1 of 4N):
+// A = p u q and B = r u s split by one flip each, A_lo_j = min(p_j, q_{N-1-j})
+// = the N smallest of A (bitonic), A_hi the N largest; the same choice as
+// above between A_hi u B_lo and A_lo u B_hi; then two_set_median.  Against
+// merging p, q and r, s into sorted halves (two Batcher merges of N + N) and
+// the pruned final merge, this drops ~2N log2 N comparators.
+template <int N, typename T>
+__device__ __forceinline__ T four_list_median(const T (&p)[N], const T (&q)[N], const T (&r)[N], const T (&s)[N]) {
+  // max_j min(p_j, q_{N-1-j}) as a v_max3 chain: the N mins are consumed as
+  // they are made (a tree would hold 2N more values live next to the lists)
+  T ma = min(p[0], q[N - 1]), mb = min(r[0], s[N - 1]);
+#pragma unroll
+  for (int j = 1; j < N; j += 2) {
+    ma = j + 1 < N ? max(max(ma, min(p[j], q[N - 1 - j])), min(p[j + 1], q[N - 2 - j])) : max(ma, min(p[j], q[N - 1 - j]));
+    mb = j + 1 < N ? max(max(mb, min(r[j], s[N - 1 - j])), min(r[j + 1], s[N - 2 - j])) : max(mb, min(r[j], s[N - 1 - j]));
+  }
+  const bool d = le(ma, mb);
+  const T lx = keep_limit(T{}, d), ly = keep_limit(T{}, !d);
+  T x[N], y[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    x[j] = keep(p[j], q[N - 1 - j], lx);
+    y[j] = keep(r[j], s[N - 1 - j], ly);
+  }
+  return two_set_median<N>(x, y);
+}
 
 template <int KP, bool ASC = true, typename T> __device__ __forceinline__ void sort_full(T (&v)[KP]) {
   if constexpr (KP == 2) net_sort2<ASC>(v);

@@ -89,42 +89,6 @@ __device__ __forceinline__ void store_half(Img im, const T (&x)[kHalf], int lane
     im[g * 64 + lane] = u32x4{raw(x[4 * g]), raw(x[4 * g + 1]), raw(x[4 * g + 2]), raw(x[4 * g + 3])};
 }
 
-// median: max_j min(B_j, A_{127-j}), A read from the image in T's domain.
-template <typename T>
-__device__ __forceinline__ float median_final(Img im, const T (&b)[kHalf], int lane) {
-  T m{};
-#pragma unroll
-  for (int g = 0; g < kHalf / 4; ++g) {
-    const u32x4 a4 = im[(kHalf / 4 - 1 - g) * 64 + lane];  // A_{127-4g-k} = word 3-k
-    const T l0 = min(b[4 * g], from_raw<T>(a4[3])), l1 = min(b[4 * g + 1], from_raw<T>(a4[2]));
-    const T l2 = min(b[4 * g + 2], from_raw<T>(a4[1])), l3 = min(b[4 * g + 3], from_raw<T>(a4[0]));
-    const T q = max(max(l0, l1), max(l2, l3));
-    m = g == 0 ? q : max(m, q);
-    if (g % kReadAhead == kReadAhead - 1) fence_after(m);  // bound the reads in flight
-  }
-  return val(m);
-}
-
-// median, split: this wave's sorted half X (registers) against the other
-// wave's half Y, of which the image holds groups 16..31 (elements 64..127):
-// max over X's groups 0..15 of min(X_j, Y_{127-j}).  Wave 1 (X = B) covers
-// j = 0..63, wave 0 (X = A, Y = B) covers the symmetric pairs (A_i, B_{127-i})
-// for i = 0..63, i.e. j = 64..127 -- together every L_j once.
-template <typename T>
-__device__ __forceinline__ T median_half(Img im, const T (&x)[kHalf], int lane) {
-  T m{};
-#pragma unroll
-  for (int g = 0; g < kHalf / 8; ++g) {
-    const u32x4 y4 = im[(kHalf / 8 - 1 - g) * 64 + lane];  // Y_{127-4g-k} = word 3-k of slot 15-g
-    const T l0 = min(x[4 * g], from_raw<T>(y4[3])), l1 = min(x[4 * g + 1], from_raw<T>(y4[2]));
-    const T l2 = min(x[4 * g + 2], from_raw<T>(y4[1])), l3 = min(x[4 * g + 3], from_raw<T>(y4[0]));
-    const T q = max(max(l0, l1), max(l2, l3));
-    m = g == 0 ? q : max(m, q);
-    if (g % kReadAhead == kReadAhead - 1) fence_after(m);
-  }
-  return m;
-}
-
 // trimmed, split flip: this wave's half X against the other's upper half Y
 // (in `other`): for i < 64, lo/hi of (X_i, Y_{127-i}); KEEP_LO keeps lo at
 // X_i and parks hi at X_{64+i} (the upper half, already handed over), else
@@ -184,18 +148,76 @@ __device__ __forceinline__ void block_sync() {
 // Pins a sorted half where it is computed.  Without a use on both sides of
 // the role branches LLVM sinks the network into one successor piecemeal, which
 // scrambles its order (a 128-key sort then holds ~250 VGPRs instead of ~135).
-template <typename T>
-__device__ __forceinline__ void pin(const T (&x)[kHalf]) {
+template <int N, typename T>
+__device__ __forceinline__ void pin(const T (&x)[N]) {
 #pragma unroll
-  for (int j = 0; j < kHalf; ++j) asm volatile("" ::"v"(raw(x[j])));
+  for (int j = 0; j < N; ++j) asm volatile("" ::"v"(raw(x[j])));
 }
 
 // One half sorted in T's domain (the block's: keys if either half holds a
-// NaN); returns the aggregate, valid where `own`.  Both waves pass the same
+// NaN); returns the aggregate, valid in wave 0.  Both waves pass the same
 // number of block barriers.
 template <int RULE>
 __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int64_t c0, uint32_t lane_off, Img im,
                                                      int h, int lane);
+
+// MEDIAN (rank 127 of 256) without sorting the halves: wave h sorts its
+// peers as two lists of 64 (p = peers 128h..128h+63, q = the next 64) and
+// splits its 128 by one flip, lo_j = min(p_j, q_{63-j}) (the 64 smallest,
+// bitonic) / hi_j = max(...).  The waves swap max(lo) (barrier 1) and both
+// make the same choice: A_hi u B_lo if max(A_lo) <= max(B_lo), else
+// A_lo u B_hi.  Wave 1 builds its half of that choice as one v_med3 per key
+// and hands it over (16 KB, barrier 2); wave 0 builds its own and runs the
+// two-set search (robust_nets.h).  Against two Batcher sorts of 128 and the
+// flip this issues 17% fewer VALU instructions per coordinate; the 16 KB
+// image leaves room for 3 blocks' worth of waves per SIMD pair.
+template <typename T, bool FLAGS = false>
+__device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im, int h, int lane,
+                                             int __attribute__((address_space(3)))* flags = nullptr, bool nan = false,
+                                             const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0) {
+  constexpr int Q = kHalf / 2;  // 64 keys per sorted list
+  T p[Q], q[Q];
+#pragma unroll
+  for (int j = 0; j < Q; ++j) {
+    p[j] = from_bits<T>(v[j]);
+    q[j] = from_bits<T>(v[Q + j]);
+  }
+  sort_full<Q>(p);
+  sort_full<Q>(q);
+  pin(p);
+  pin(q);
+  // max_j min(p_j, q_{63-j}) as a v_max3 chain (the mins consumed as made)
+  T m = min(p[0], q[Q - 1]);
+#pragma unroll
+  for (int j = 1; j + 1 < Q; j += 2) m = max(max(m, min(p[j], q[Q - 1 - j])), min(p[j + 1], q[Q - 2 - j]));
+  m = max(m, min(p[Q - 1], q[0]));
+  auto part = (uint32_t __attribute__((address_space(3)))*)(im + Q / 4 * 64);  // max(lo) of wave h at [64h + lane]
+  part[h * 64 + lane] = raw(m);
+  if constexpr (FLAGS) {
+    if (lane == 0) flags[h] = nan ? 1 : 0;
+  }
+  block_sync();  // 1: both max(lo)
+  if constexpr (FLAGS) {
+    if (uniform((flags[0] | flags[1]) != 0)) return pair_keys<P2P_RULE_MEDIAN>(P, c0, lane_off, im, h, lane);
+  }
+  const T mo = from_raw<T>(part[(1 - h) * 64 + lane]);
+  const bool d = h == 0 ? le(m, mo) : le(mo, m);  // max(A_lo) <= max(B_lo): A_hi u B_lo
+  // wave 0 keeps A_hi (d) / A_lo; wave 1 keeps B_lo (d) / B_hi: the top limit iff d == (h == 0)
+  const T lim = keep_limit(T{}, d == (h == 0));
+  T x[Q];
+#pragma unroll
+  for (int j = 0; j < Q; ++j) x[j] = keep(p[j], q[Q - 1 - j], lim);
+  if (h == 1) {
+#pragma unroll
+    for (int g = 0; g < Q / 4; ++g) im[g * 64 + lane] = u32x4{raw(x[4 * g]), raw(x[4 * g + 1]), raw(x[4 * g + 2]), raw(x[4 * g + 3])};
+  }
+  block_sync();  // 2: B's kept half in the image
+  if (h == 1) return 0.f;
+  T y[Q];
+#pragma unroll
+  for (int j = 0; j < Q; ++j) y[j] = from_raw<T>(img_at(im, j, lane));
+  return val(two_set_median<Q>(x, y));
+}
 
 // FLAGS (float path): the two waves swap "my half holds a NaN" at barrier 1,
 // beside the hand-off; a block that finds one re-runs the tile on the key
@@ -225,14 +247,7 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   if constexpr (FLAGS) {
     if (uniform((flags[0] | flags[1]) != 0)) return pair_keys<RULE>(P, c0, lane_off, im, h, lane);
   }
-  if constexpr (RULE == P2P_RULE_MEDIAN) {
-    // wave 1 pairs its B with A's upper half, wave 0 its A with B's upper half
-    auto part = (float __attribute__((address_space(3)))*)(im + kHalf / 4 * 64);
-    const T m = median_half(im + (h == 0 ? kHalf / 8 * 64 : 0), x, lane);
-    if (h == 0) part[lane] = __uint_as_float(raw(m));
-    block_sync();  // 2: wave 0's partial max in its slot
-    return h == 1 ? val(max(m, from_raw<T>(__float_as_uint(part[lane])))) : 0.f;
-  } else {
+  {
     constexpr int b = (2 * kHalf * 2) / 10;  // 51
     constexpr int hi = 2 * kHalf - b;        // 205: ranks b..hi-1 kept
     constexpr int Q = kHalf / 2;             // 64
@@ -298,19 +313,18 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
   h = __builtin_amdgcn_readfirstlane(h);
   uint32_t v[kHalf];
   load_half(v, P, c0, lane_off, h);
-  return pair_body<RULE, uint32_t>(v, im, h, lane);
+  if constexpr (RULE == P2P_RULE_MEDIAN) return median_pair<uint32_t>(v, im, h, lane);
+  else return pair_body<RULE, uint32_t>(v, im, h, lane);
 }
 
-// SMALL (flat buffers below 2^30 floats): the tile start rides in the 32-bit
-// lane offset and each peer row's pointer is the scalar base as loaded -- no
-// 64-bit scalar add per load (256 SALU instructions per wave and tile).
-template <int RULE, bool SEGS, bool SMALL = false>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(const float* const* __restrict__ peers,
-                                                          const Seg* __restrict__ segs, int nseg, int64_t n,
-                                                          float* w, float* out, float lr) {
-  __shared__ u32x4 img_raw[kHalf / 4 * 64 + 16];  // 32 KB image + the trimmed mean's partial sums (256 B)
-  __shared__ int nan_flag[2];
-  Img im = (Img)img_raw;
+// One 64-coordinate tile of the pair kernels.  SMALL (flat buffers below
+// 2^30 floats): the tile start rides in the 32-bit lane offset and each peer
+// row's pointer is the scalar base as loaded -- no 64-bit scalar add per load
+// (256 SALU instructions per wave and tile).
+template <int RULE, bool SEGS, bool SMALL>
+__device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers, const Seg* __restrict__ segs,
+                                          int nseg, int64_t n, float* w, float* out, float lr, Img im,
+                                          int __attribute__((address_space(3)))* flags) {
   const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
   const int lane = tid_x() & 63;
   const int64_t t = bid_x();
@@ -333,15 +347,38 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
   uint32_t v[kHalf];
   load_half(v, P, cb, lane_off, h);
   // One domain per block: the float network unless either half holds a NaN
-  // (flags swapped at the hand-off barrier, no barrier of their own).
+  // (flags swapped at the first barrier, no barrier of their own).
   const bool nan = uniform(wave_has_nan(v));
-  const float agg = pair_body<RULE, fk, true>(v, im, h, lane, (int __attribute__((address_space(3)))*)nan_flag, nan,
-                                              P, cb, lane_off);
-  const bool own = RULE == P2P_RULE_MEDIAN ? h == 1 : h == 0;
-  if (own && i < N) {
+  float agg;
+  if constexpr (RULE == P2P_RULE_MEDIAN) agg = median_pair<fk, true>(v, im, h, lane, flags, nan, P, cb, lane_off);
+  else agg = pair_body<RULE, fk, true>(v, im, h, lane, flags, nan, P, cb, lane_off);
+  if (h == 0 && i < N) {  // wave 0 holds the aggregate
     if (O) stg(O + i, agg);
     if (W) stg(W + i, apply_lr(ldg(W + i), lr, agg));
   }
+}
+
+// Trimmed mean: 32 KB image + the partial sums (256 B), 2 waves per SIMD.
+template <bool SEGS, bool SMALL = false>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(
+    const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n, float* w,
+    float* out, float lr) {
+  __shared__ u32x4 img_raw[kHalf / 4 * 64 + 16];
+  __shared__ int nan_flag[2];
+  pair_tile<P2P_RULE_TRIMMED, SEGS, SMALL>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
+                                           (int __attribute__((address_space(3)))*)nan_flag);
+}
+
+// Median: 16 KB image (B's kept half) + both max(lo) (512 B), 3 waves per
+// SIMD (<= 168 VGPRs).
+template <bool SEGS, bool SMALL = false>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void robust_median_pair_kernel(
+    const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n, float* w,
+    float* out, float lr) {
+  __shared__ u32x4 img_raw[kHalf / 8 * 64 + 32];
+  __shared__ int nan_flag[2];
+  pair_tile<P2P_RULE_MEDIAN, SEGS, SMALL>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
+                                          (int __attribute__((address_space(3)))*)nan_flag);
 }
 
 }  // namespace p2p
@@ -358,12 +395,12 @@ extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, c
   if (grid <= 0) return;
   const dim3 g(static_cast<unsigned>(grid)), b(2 * 64);
   if (rule == P2P_RULE_MEDIAN) {
-    if (segs) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, false, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_MEDIAN, false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    if (segs) hipLaunchKernelGGL((robust_median_pair_kernel<true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_median_pair_kernel<false, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    else hipLaunchKernelGGL((robust_median_pair_kernel<false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
   } else {
-    if (segs) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, false, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else hipLaunchKernelGGL((robust_pair_kernel<P2P_RULE_TRIMMED, false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    if (segs) hipLaunchKernelGGL((robust_pair_kernel<true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_pair_kernel<false, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    else hipLaunchKernelGGL((robust_pair_kernel<false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
   }
 }

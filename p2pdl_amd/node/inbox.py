@@ -127,12 +127,11 @@ def _run_pickle(mv: memoryview, pos: int, *, min_proto: int, resolve_global, per
         need(p, k)
         return mv[p:p + k]
 
-    def pop_mark():
-        nonlocal stack
+    def pop_mark():  # in place: the rest of the stack is never copied
         for i in range(len(stack) - 1, -1, -1):
             if stack[i] is _MARK:
                 items = stack[i + 1:]
-                stack = stack[:i]
+                del stack[i:]
                 return items
         raise pickle.UnpicklingError("MARK not found")
 
@@ -367,6 +366,16 @@ def _rebuild_tensor_v2(storage, offset, size, stride, requires_grad=False, hooks
         last = offset + sum((s - 1) * st for s, st in zip(size, stride))
         if last >= storage.numel:
             raise pickle.UnpicklingError(f"tensor view ends at element {last}, storage holds {storage.numel}")
+        # A state_dict tensor is dense: a view repeating elements (a zero
+        # stride, or more elements than its storage holds) would make a
+        # few-byte message expand into an arbitrarily large copy.
+        if any(st == 0 and s > 1 for s, st in zip(size, stride)):
+            raise pickle.UnpicklingError("tensor view with a zero stride")
+        numel = 1
+        for s in size:
+            numel *= s
+        if numel > storage.numel - offset:
+            raise pickle.UnpicklingError(f"tensor view of {numel} elements over {storage.numel - offset}")
     elif offset > storage.numel:
         raise pickle.UnpicklingError("tensor offset past the end of its storage")
     return RawTensor(storage, offset, size, stride)
@@ -567,7 +576,22 @@ class DeviceInbox:
             self.count = max(self.count, k + 1)
             if fut is not None:
                 self._digests[k] = fut
+            else:  # a digest of the row's previous bytes must not outlive them
+                self._digests.pop(k, None)
             return self._land_locked(raw, k)
+
+    def order_after_landing(self, stream=None) -> None:
+        """Make ``stream`` (default: the current stream of the slab's device)
+        wait for the row copies issued by ``land`` -- they run on the landing
+        thread's stream -- so a kernel launched on it reads the landed bytes.
+        Device-side waits only; the host does not block."""
+        with self._lock:
+            events = [e for e in self._events if e is not None]
+        if not events:
+            return
+        stream = stream or torch.cuda.current_stream(self.device)
+        for ev in events:
+            stream.wait_event(ev)
 
     def digest(self, k: int) -> bytes:
         """SHA-256 of the bytes landed in row k with ``land(..., digest=True)``

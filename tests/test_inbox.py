@@ -200,6 +200,38 @@ def test_out_of_bounds_tensor_views_are_refused(view):
             parse(data)
 
 
+@pytest.mark.parametrize("view", [
+    dict(size=(2 ** 33,), stride=(0,)),       # 8 G elements over one storage element
+    dict(size=(2, 3), stride=(0, 1)),         # a repeated row
+    dict(size=(3, 3), stride=(1, 1)),         # overlapping rows, 9 elements over 5
+])
+def test_repeating_tensor_views_are_refused(view):
+    """a zero-stride / overlapping view inside its
+    storage passed the bounds check, and a key outside the fp32 template was
+    then copied element by element -- a few hundred bytes asking for 32 GB."""
+    data = _forged(_good_blob(5), **view)
+    for parse in PARSERS:
+        with pytest.raises(pickle.UnpicklingError):
+            parse(data)
+    # dense views of every shape still parse, incl. size-1 dims with any stride
+    for ok in (dict(size=(5,)), dict(size=(1, 5), stride=(0, 1)), dict(size=(5, 1), stride=(1, 0))):
+        raw = ZeroCopyParser(_forged(_good_blob(5), **ok)).parse()
+        assert raw["a"].array().size == 5
+
+
+def test_many_marks_parse_in_linear_time():
+    """closing a MARK copied the rest of the stack (O(n^2) in a
+    listener thread for a message of MARK ... TUPLE pairs)."""
+    import time
+
+    n = 200_000
+    body = b"\x80\x04" + b"(" * n + b")" + b"t" * n + b"."  # PROTO 4, n MARKs, EMPTY_TUPLE, n TUPLEs
+    t0 = time.perf_counter()
+    with pytest.raises(pickle.UnpicklingError):  # well-formed, but not a state_dict
+        ZeroCopyParser(body).parse()
+    assert time.perf_counter() - t0 < 5.0
+
+
 def test_build_cannot_shadow_dict_methods():
     """A pickle's BUILD on the OrderedDict may set only torch's `_metadata`."""
     class Shadow(collections.OrderedDict):
@@ -400,6 +432,9 @@ def test_device_inbox_digest_overlapped_with_landing(cuda):
     inbox.land(ser[0], k)
     with pytest.raises(KeyError):
         inbox.digest(k)
+    inbox.land(ser[1], 0)  # re-landed without a digest, row 0's old one is gone
+    with pytest.raises(KeyError):
+        inbox.digest(0)
     inbox.reset()
     with pytest.raises(KeyError):
         inbox.digest(0)
@@ -494,11 +529,27 @@ def test_slab_table_cache_across_rounds_and_streams(cuda, monkeypatch):
     node = types.SimpleNamespace(model=model, trainers_list=[0] * k, addr="a", port=1, neighbors=[],
                                  received_models=[])
     w = w0
+    side = torch.cuda.Stream(cuda)
     for rnd, (rows, stream) in enumerate([(range(k), None), (range(k), None), (range(1, k + 1), None),
-                                          (range(1, k + 1), torch.cuda.Stream(cuda))]):
+                                          (range(1, k + 1), torch.cuda.Stream(cuda)), (range(k), "land")]):
         inbox.reset()
         ser = [pickle.dumps(mlp_update(90 + 10 * rnd + j)) for j in range(k)]
-        landed = [inbox.land(s, r) for s, r in zip(ser, rows)]
+        if stream == "land":
+            # a listener thread lands on its own stream; the
+            # aggregator launches on its current stream with no sync of its own
+            landed = [None] * k
+
+            def listener():
+                with torch.cuda.stream(side):
+                    for j, (s_, r) in enumerate(zip(ser, rows)):
+                        landed[j] = inbox.land(s_, r)
+
+            th = threading.Thread(target=listener)
+            th.start()
+            th.join(60)
+            stream = None
+        else:
+            landed = [inbox.land(s_, r) for s_, r in zip(ser, rows)]
         node.received_models = [{"model": u, "sender": j} for j, u in enumerate(landed)]
         flat = [np.concatenate([pickle.loads(s)[name].numpy().reshape(-1) for name, _ in MLP_SHAPES])
                 for s in ser]

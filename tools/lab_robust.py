@@ -42,8 +42,6 @@ def main():
     lib.p2p_lab_robust.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                                    ctypes.c_int32, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.p2p_lab_robust.restype = ctypes.c_int32
-    lib.p2p_lab_fallbacks.argtypes = [ctypes.c_int32]
-    lib.p2p_lab_fallbacks.restype = ctypes.c_int64
     dev = torch.device("cuda", 0)
     K, n = a.peers, a.coords
     slab = torch.empty((K, n), dtype=torch.float32, device=dev)
@@ -73,7 +71,6 @@ def main():
             print(json.dumps({"variant": v, "error": rc}), flush=True)
             continue
         torch.cuda.synchronize()
-        lib.p2p_lab_fallbacks(1)
         ev = []
         for _ in range(a.steps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -82,7 +79,6 @@ def main():
             e1.record(stream)
             ev.append((e0, e1))
         torch.cuda.synchronize()
-        fb = lib.p2p_lab_fallbacks(1)
         ms = sorted(x.elapsed_time(y) for x, y in ev)
         med = ms[len(ms) // 2]
         outs[v] = out
@@ -94,12 +90,9 @@ def main():
                 bad = (o0 != out.view(torch.int32)).nonzero()
                 same = f"MISMATCH at {bad.numel()} coords, first {bad[:4].flatten().tolist()}"
         alg = 4 * n * (K + 2)
-        waves = -(-n // (32 if v == 1 else 16))
         print(json.dumps({"variant": v, "rule": a.rule, "peers": K, "coords": n, "data": a.data,
                           "ms_median": round(med, 3), "ms_min": round(ms[0], 3),
                           "frac_hbm": round(alg / (med / 1e3) / 1e9 / HBM, 4),
-                          "fallback_waves_per_launch": fb / a.steps if fb >= 0 else None,
-                          "fallback_frac": round(fb / a.steps / waves, 5) if fb >= 0 else None,
                           "bit_equal_to_variant0": same}), flush=True)
         del w
 

@@ -1,5 +1,5 @@
 // A/B library for the robust kernels -- NOT the product.  It compiles the
-// product's robust_lds.hip with P2P_LAB (fallback counters) and exposes the
+// product's robust_lds.hip and exposes the
 // template instantiations the product dispatch does not use, so variants can
 // be timed and bit-compared against the product kernel on the same inputs.
 // Built by `make -C p2pdl_amd/csrc lab` into tools/libp2pdl_lab.so (the
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(768) void robust_lds_g2a_kernel(const float* const*
       ++dma_seen;
       lds_wait_ge(&full[g], 4 * dma_seen);  // all four loaders' pieces landed
     } else {
-      fill_direct<L, H, 1>(im, me.peers, me.w, me.n, me.c0 + c, K, q, c);
+      fill_direct<L, H>(im, me.peers, me.w, me.n, me.c0 + c, K, q, c);
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     uint32_t v[H];
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(768) void robust_lds_g2a_kernel(const float* const*
     bool own = false;
     float agg;
     bool fast = false;  // NaN-free wave with every slot real: the float network
-    if constexpr (MODE != 0 && !P2P_NO_FLOAT_PATH) fast = !wave_has_nan(v);
+    if constexpr (MODE != 0) fast = !wave_has_nan(v);
     if (fast) {
       fk f[H];
 #pragma unroll
@@ -207,11 +207,11 @@ static void launch_lds_g2a(const LdsArgs& a) {
 
 }  // namespace p2p
 
-// variant: 0 product layout (4 lanes x 64 keys), 1 radix16 affine median
-// (K = 256 only), 2 LDS 4 x 32 (K <= 128), 3 LDS 2 x 64 (K <= 128),
+// variant: 0 the 4-lane layout (4 lanes x 64 keys), 2 LDS 4 x 32 (K <= 128), 3 LDS 2 x 64 (K <= 128),
 // 4 LDS 1 x 128 (K <= 128), 5 LDS 2 x 128 (K in 129..256), 7 two sorter groups per
 // block (K in 129..256), 8 the same, asynchronous (LDS counters); the
-// self-staged layout (variant 6, profiles/r02/ab/labself*) was removed
+// self-staged layout (variant 6, profiles/r02/ab/labself*) and the radix16
+// affine median (variant 1) were removed
 extern "C" int32_t p2p_lab_robust(int32_t variant, const float* const* peers, int32_t k, int64_t n,
                                   int32_t rule, int32_t trim_b, float lr, float* w, float* out,
                                   p2p_stream_t stream) {
@@ -220,10 +220,6 @@ extern "C" int32_t p2p_lab_robust(int32_t variant, const float* const* peers, in
   switch (variant) {
     case 0:
       if (med) launch_lds<4, 64, P2P_RULE_MEDIAN>(a); else launch_lds<4, 64, P2P_RULE_TRIMMED>(a);
-      break;
-    case 1:
-      if (!med || k != 256) return P2P_ERR_UNSUPPORTED;
-      launch_lds_kernel<4, 64, P2P_RULE_MEDIAN, 1, false, 0, 2>(a);
       break;
     case 2:
       if (k > 128) return P2P_ERR_UNSUPPORTED;
@@ -254,15 +250,4 @@ extern "C" int32_t p2p_lab_robust(int32_t variant, const float* const* peers, in
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? P2P_OK : static_cast<int32_t>(e);
-}
-
-// Waves that took the exact fallback since the last reset (radix16 variant).
-extern "C" int64_t p2p_lab_fallbacks(int32_t reset) {
-  int h[64];
-  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_lab_fallback), sizeof(h)) != hipSuccess) return -1;
-  if (reset) {
-    int z[64] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lab_fallback), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return h[0];
 }
