@@ -27,10 +27,16 @@ import logging
 import pickle
 import socket
 
+import numpy as np
 import torch
 
 from .. import ops
 from ..utils.waiting import wait_for_models
+
+try:  # host-side C gather of the peer table (p2pdl_amd/csrc/host_tables.cpp)
+    from .. import _host_tables
+except ImportError:  # not built: the per-tensor Python path (same results)
+    _host_tables = None
 
 LEARNING_RATE = 0.1       # reference aggregation.py:36
 AGGREGATION_RULE = "fedavg"
@@ -60,10 +66,15 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
         self.received_models.clear()
         broadcast_global_model_update(self)
         return
-    updates = []
-    for received_model in received:  # KeyError on a missing key, like :28
-        local_update = received_model["model"]
-        updates.append([local_update[key] for key in keys])
+    # The (L, K) peer table gathered in C when every update tensor is a plain
+    # fp32 tensor on the model's device (KeyError on a missing key, like :28);
+    # otherwise the per-tensor path below, with the exact diagnosis.
+    table = _gather_table(received, keys, state)
+    if table is None:
+        updates = []
+        for received_model in received:  # KeyError on a missing key, like :28
+            local_update = received_model["model"]
+            updates.append([local_update[key] for key in keys])
 
     for key in keys:  # the reference raises at the division for integer tensors (:32)
         t = state[key]
@@ -74,6 +85,16 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
             raise NotImplementedError(f"p2pdl_amd aggregates float32 state_dicts; {key} is {t.dtype}")
 
     ws = [state[key] for key in keys]
+    if table is not None:
+        ws_c = [w if w.is_contiguous() else w.contiguous() for w in ws]
+        ops.aggregate_ptr_table_(ws_c, table, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac)
+        for w, wc in zip(ws, ws_c):
+            if wc is not w:
+                w.copy_(wc)
+        logging.info(f"[{self.addr}:{self.port}] Model aggregation completed, applied local updates.")
+        self.received_models.clear()
+        broadcast_global_model_update(self)
+        return
     numels = [w.numel() for w in ws]
     dev = ws[0].device if ws else None
     di = dev.index if dev is not None else None
@@ -102,6 +123,22 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
 
     # Broadcast the newly aggregated global model (:46)
     broadcast_global_model_update(self)
+
+
+def _gather_table(received, keys, state):
+    """uint64 [L, K] device addresses of received[j]["model"][key], or None
+    when the C gather cannot vouch for every tensor (not fp32 / contiguous /
+    on the model's CUDA device / the parameter's element count) -- the
+    caller's per-tensor path then diagnoses or widens exactly as before."""
+    if _host_tables is None or not keys:
+        return None
+    ws = [state[key] for key in keys]
+    dev = ws[0].device
+    if dev.type != "cuda":
+        return None
+    table = np.empty((len(keys), len(received)), dtype=np.uint64)
+    status = _host_tables.gather_peer_table(received, keys, [w.numel() for w in ws], dev.index, table)
+    return table if status == 0 else None
 
 
 def _checked_update(j, key, w, u):

@@ -1,0 +1,118 @@
+// Host side of the drop-in's general path: the (L, K) peer-pointer table of
+// aggregate_models (reference aggregator/aggregation.py:25-28 reads
+// received_models[j]["model"][key] for every key of self.model.state_dict()
+// and every update j).  With plain dicts of tensors -- what the reference's
+// listener appends after pickle.loads (node/node.py:135-141) -- the Python
+// loop cost ~0.5 us per tensor in dict lookups and dtype / device / layout
+// getters: 1.9 ms per call for ResNet-18 x 64 updates, 3.7x the kernel.  This
+// walks the same lists in C (CPython dict lookups, ATen getters) and writes
+// the table straight into the caller's buffer.
+//
+// gather_peer_table(received, keys, numels, device, out) -> int
+//   received : list of update records; record["model"][key] is the tensor
+//              (the reference's lookups, KeyError on a missing one)
+//   keys     : list of L state_dict keys; numels: L element counts
+//   device   : CUDA device index of the model
+//   out      : writable buffer of L*K uint64, row-major [l][j]
+// Returns 0 with out filled when every tensor is fp32, contiguous, on
+// `device` with numels[l] elements; 1 (out partially written, nothing
+// raised) when some tensor needs the Python path's exact diagnosis or
+// widening; raises what the reference's lookups raise (KeyError, TypeError).
+#include <Python.h>
+
+#include <ATen/core/Tensor.h>
+#include <torch/csrc/autograd/python_variable.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace {
+
+PyObject* g_model_key = nullptr;  // interned "model"
+
+// record[key] with the reference's semantics: exact dicts through the dict
+// API, any other mapping through __getitem__; a new reference or nullptr.
+PyObject* get_item(PyObject* mapping, PyObject* key) {
+  if (PyDict_CheckExact(mapping)) {
+    PyObject* v = PyDict_GetItemWithError(mapping, key);
+    if (v) {
+      Py_INCREF(v);
+      return v;
+    }
+    if (!PyErr_Occurred()) PyErr_SetObject(PyExc_KeyError, key);
+    return nullptr;
+  }
+  return PyObject_GetItem(mapping, key);
+}
+
+PyObject* gather_peer_table(PyObject*, PyObject* args) {
+  PyObject *received, *keys, *numels_obj;
+  int device;
+  Py_buffer out;
+  if (!PyArg_ParseTuple(args, "O!O!O!iw*", &PyList_Type, &received, &PyList_Type, &keys, &PyList_Type,
+                        &numels_obj, &device, &out))
+    return nullptr;
+  const Py_ssize_t K = PyList_GET_SIZE(received), L = PyList_GET_SIZE(keys);
+  int status = 0;
+  std::vector<int64_t> numels(static_cast<size_t>(L));
+  for (Py_ssize_t l = 0; l < L; ++l) {
+    numels[l] = PyLong_AsLongLong(PyList_GET_ITEM(numels_obj, l));
+    if (numels[l] == -1 && PyErr_Occurred()) {
+      PyBuffer_Release(&out);
+      return nullptr;
+    }
+  }
+  if (out.len < static_cast<Py_ssize_t>(sizeof(uint64_t)) * L * K || PyList_GET_SIZE(numels_obj) != L) {
+    PyBuffer_Release(&out);
+    PyErr_SetString(PyExc_ValueError, "gather_peer_table: buffer / numels do not match L x K");
+    return nullptr;
+  }
+  uint64_t* table = static_cast<uint64_t*>(out.buf);
+  for (Py_ssize_t j = 0; j < K && status == 0; ++j) {
+    PyObject* model = get_item(PyList_GET_ITEM(received, j), g_model_key);
+    if (!model) {
+      PyBuffer_Release(&out);
+      return nullptr;
+    }
+    for (Py_ssize_t l = 0; l < L; ++l) {
+      PyObject* t = get_item(model, PyList_GET_ITEM(keys, l));
+      if (!t) {
+        Py_DECREF(model);
+        PyBuffer_Release(&out);
+        return nullptr;
+      }
+      if (!THPVariable_Check(t)) {
+        Py_DECREF(t);
+        status = 1;  // not a tensor: the Python path reports it the reference's way
+        break;
+      }
+      const at::Tensor& x = THPVariable_Unpack(t);
+      if (x.scalar_type() != at::kFloat || !x.is_cuda() || x.get_device() != device || !x.is_contiguous() ||
+          x.numel() != numels[l]) {
+        Py_DECREF(t);
+        status = 1;
+        break;
+      }
+      table[l * K + j] = reinterpret_cast<uint64_t>(x.data_ptr());
+      Py_DECREF(t);
+    }
+    Py_DECREF(model);
+  }
+  PyBuffer_Release(&out);
+  return PyLong_FromLong(status);
+}
+
+PyMethodDef methods[] = {
+    {"gather_peer_table", gather_peer_table, METH_VARARGS,
+     "gather_peer_table(received, keys, numels, device, out) -> 0 (table filled) or 1 (use the Python path)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef module = {PyModuleDef_HEAD_INIT, "_host_tables", nullptr, -1, methods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__host_tables(void) {
+  g_model_key = PyUnicode_InternFromString("model");
+  if (!g_model_key) return nullptr;
+  return PyModule_Create(&module);
+}

@@ -292,6 +292,44 @@ def aggregate_segments_(ws: Sequence[torch.Tensor], peer_lists: Sequence[Sequenc
     _launch_segments(ws, ptrs, numels, rule, K, lr, trim_b, trim_frac, outs, dev)
 
 
+def aggregate_ptr_table_(ws: Sequence[torch.Tensor], ptrs: np.ndarray, rule="fedavg", *, lr: float = 0.1,
+                         trim_b: int | None = None, trim_frac: float = DEFAULT_TRIM_FRAC) -> None:
+    """aggregate_segments_ for a peer-pointer table the caller has already
+    gathered and validated: ptrs[l, j] = device address of update j's
+    fp32 tensor for key l (ws[l].numel() elements each, contiguous, on ws'
+    device) -- what _host_tables.gather_peer_table returns for
+    aggregate_models' general path.  The device table is cached by the
+    addresses and sizes it encodes (a round whose updates land at the same
+    addresses reuses it, as aggregate_slab_rows_ does)."""
+    L = len(ws)
+    if L == 0:
+        return
+    if ptrs.shape[0] != L or ptrs.shape[1] == 0 or ptrs.dtype != np.uint64:
+        raise ValueError("ptrs must be a uint64 [L, K] table, K >= 1")
+    K = ptrs.shape[1]
+    dev = ws[0].device
+    N.require_device(ws[0])
+    numels = []
+    for l, w in enumerate(ws):
+        _check_f32(w, f"w[{l}]", dev)
+        numels.append(w.numel())
+    key = (dev.index, "ptrs", ptrs.tobytes(), tuple(w.data_ptr() for w in ws), tuple(numels), rule_id(rule), K,
+           trim_b, float(trim_frac))
+    with _TABLES_LOCK:
+        hit = _TABLES.get(key)
+        if hit is not None:
+            _TABLES.move_to_end(key)
+    if hit is not None:
+        buf, tiles, r, b, alloc_stream = hit
+        with torch.cuda.device(dev) if torch.cuda.current_device() != dev.index else _NO_CTX:
+            stream = torch.cuda.current_stream(dev)
+            if stream.cuda_stream != alloc_stream:
+                buf.record_stream(stream)
+            _launch_table(buf.data_ptr(), L, tiles, K, r, b, lr)
+        return
+    _launch_segments(ws, ptrs, numels, rule, K, lr, trim_b, trim_frac, None, dev, cache_key=key)
+
+
 def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: Sequence[int],
                          offsets: Sequence[int], rule="fedavg", *, lr: float = 0.1,
                          trim_b: int | None = None, trim_frac: float = DEFAULT_TRIM_FRAC) -> None:

@@ -220,6 +220,67 @@ def test_dropin_cfg2_resnet18_full_size(cuda, rule, monkeypatch):
     assert node.received_models == []
 
 
+def test_dropin_plain_dicts_take_the_c_gather(cuda, monkeypatch):
+    """plain dicts of fp32 CUDA tensors (what pickle.loads
+    gives the reference's listener, node/node.py:135-141) reach the kernel
+    through the C gather of the peer table (p2pdl_amd/csrc/host_tables.cpp),
+    bit-exact; a second round at the same addresses reuses the device table;
+    a missing key raises KeyError before anything changes (reference :28);
+    a non-contiguous update takes the per-tensor path, same bits."""
+    from p2pdl_amd import _host_tables  # noqa: F401  (built in-tree: the fast host path must exist)
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
+    shapes = [("fc1.weight", (64, 48)), ("fc1.bias", (64,)), ("fc2.weight", (10, 64)), ("fc2.bias", (10,))]
+    n = sum(int(np.prod(s)) for _, s in shapes)
+    k = 5
+    w0 = oracle.synth(n, 41, 0xFFFFF, 5e-2)
+    peers = [oracle.synth(n, 41, p, 1e-2) for p in range(k)]
+    want, _ = oracle.fedavg(peers, w0)
+    want2, _ = oracle.fedavg(peers, want)
+
+    def boom(*a, **kw):
+        raise AssertionError("per-tensor path taken")
+
+    model = Holder(shapes).to(cuda)
+    with torch.no_grad():
+        model.load_state_dict(split(w0, shapes, cuda))
+    upd = [split(p, shapes, cuda) for p in peers]
+    calls = []
+    real = ops.aggregate_ptr_table_
+    monkeypatch.setattr(ops, "aggregate_ptr_table_", lambda *a, **kw: (calls.append(1), real(*a, **kw)))
+    with monkeypatch.context() as m:
+        m.setattr(ops, "aggregate_segments_", boom)
+        agg.aggregate_models(fake_node(model, upd))
+        got = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+        assert_bits_equal(got, want, what="C gather round 1")
+        before = len(ops._TABLES)
+        agg.aggregate_models(fake_node(model, upd))  # same tensors, same addresses: cached table
+        assert len(ops._TABLES) == before
+        got = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+        assert_bits_equal(got, want2, what="C gather round 2")
+    assert len(calls) == 2
+    missing = [dict(u) for u in upd]
+    del missing[3]["fc2.bias"]
+    node = fake_node(model, missing)
+    with pytest.raises(KeyError):
+        agg.aggregate_models(node)
+    assert len(node.received_models) == k
+    got = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+    assert_bits_equal(got, want2, what="unchanged after KeyError")
+    # a transposed (non-contiguous) view of the same values: per-tensor path
+    with torch.no_grad():
+        model.load_state_dict(split(w0, shapes, cuda))
+    odd = [dict(u) for u in upd]
+    odd[1]["fc1.weight"] = odd[1]["fc1.weight"].t().contiguous().t()
+    assert not odd[1]["fc1.weight"].is_contiguous()
+    calls.clear()
+    agg.aggregate_models(fake_node(model, odd))
+    assert calls == []
+    got = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+    assert_bits_equal(got, want, what="non-contiguous update")
+
+
 def test_dropin_widens_half_updates_and_rejects_float64(cuda, monkeypatch):
     """fp16 / bf16 updates widen to fp32 exactly (what the reference's fp32
     `acc += u` computes in); fp64 updates are refused -- the reference adds
