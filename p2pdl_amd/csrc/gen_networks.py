@@ -2,9 +2,9 @@
 """Generate register-resident sorting / selection networks for robust.hip.
 
 Each network sorts (or partially sorts) KP uint32 keys held in a fully
-unrolled register array.  The base network is Batcher's odd-even merge sort
-(fewest comparators of the simple power-of-two constructions: 1471 for 128,
-3839 for 256).  For a fixed set of wanted output ranks the network is pruned
+unrolled register array.  The base network sorts blocks of 16 with a
+60-comparator network and merges them with Batcher's odd-even merges (1447
+comparators for 128 against 1471 for Batcher's odd-even merge sort).  For a fixed set of wanted output ranks the network is pruned
 backwards: a comparator whose two outputs are both dead is dropped, one with a
 single live output becomes a lone v_min_u32 / v_max_u32.
 
@@ -37,6 +37,48 @@ def batcher(n: int):
             k //= 2
         p *= 2
     return comps
+
+
+# A 16-input sorting network of 60 comparators in 10 layers (Green's count;
+# Batcher's odd-even merge sort needs 63), checked exhaustively on all 2^16
+# 0-1 inputs by --check.
+GREEN16 = [
+    [(0, 13), (1, 12), (2, 15), (3, 14), (4, 8), (5, 6), (7, 11), (9, 10)],
+    [(0, 5), (1, 7), (2, 9), (3, 4), (6, 13), (8, 14), (10, 15), (11, 12)],
+    [(0, 1), (2, 3), (4, 5), (6, 8), (7, 9), (10, 11), (12, 13), (14, 15)],
+    [(0, 2), (1, 3), (4, 10), (5, 11), (6, 7), (8, 9), (12, 14), (13, 15)],
+    [(1, 2), (3, 12), (4, 6), (5, 7), (8, 10), (9, 11), (13, 14)],
+    [(1, 4), (2, 6), (5, 8), (7, 10), (9, 13), (11, 14)],
+    [(2, 4), (3, 6), (9, 12), (11, 13)],
+    [(3, 5), (6, 8), (7, 9), (10, 12)],
+    [(3, 4), (5, 6), (7, 8), (9, 10), (11, 12)],
+    [(6, 7), (8, 9)],
+]
+
+
+def oddeven_merge(lo: int, hi: int, r: int):
+    """Batcher's odd-even merge of the two sorted halves of [lo, hi] (hi
+    inclusive) taken with stride r."""
+    step = 2 * r
+    if step < hi - lo:
+        yield from oddeven_merge(lo, hi, step)
+        yield from oddeven_merge(lo + r, hi, step)
+        for i in range(lo + r, hi - r, step):
+            yield (i, i + r)
+    else:
+        yield (lo, lo + r)
+
+
+def green_batcher(n: int, lo: int = 0):
+    """Sort n = 2^k keys at [lo, lo + n): the 60-comparator network on each
+    block of 16, then Batcher's odd-even merges (32: 185, 64: 531, 128: 1447
+    comparators against 191 / 543 / 1471)."""
+    if n <= 8:
+        return [(lo + a, lo + b) for a, b in batcher(n)]
+    if n == 16:
+        return [(lo + a, lo + b) for layer in GREEN16 for a, b in layer]
+    h = n // 2
+    return green_batcher(h, lo) + green_batcher(h, lo + h) + list(oddeven_merge(lo, lo + n - 1, 1))
 
 
 def prune(comps, wanted):
@@ -87,7 +129,7 @@ def bitonic_merge(n: int):
     return comps
 
 
-NETWORKS = {"batcher": batcher, "bmerge": bitonic_merge}
+NETWORKS = {"batcher": batcher, "bmerge": bitonic_merge, "green": green_batcher}
 
 
 def network_specs():
@@ -101,14 +143,14 @@ def network_specs():
     pruned 128-key networks serve the single-lane K in 65..128 variant."""
     specs = []
     for kp in (2, 4, 8, 16, 32, 64, 128):
-        specs.append((f"sort{kp}", kp, None, "batcher"))
+        specs.append((f"sort{kp}", kp, None, "green"))
     for kp in (32, 64, 128):
         specs.append((f"bmerge{kp}", kp, None, "bmerge"))
     # specialised K == KP instances for the benchmark configurations
     for kp in (64, 128):
-        specs.append((f"median{kp}", kp, [(kp - 1) // 2], "batcher"))
+        specs.append((f"median{kp}", kp, [(kp - 1) // 2], "green"))
         b = int(0.2 * kp + 1e-9)
-        specs.append((f"trim{kp}_b{b}", kp, list(range(b, kp - b)), "batcher"))
+        specs.append((f"trim{kp}_b{b}", kp, list(range(b, kp - b)), "green"))
     # trimmed mean of 256 in one lane per coordinate (robust_pair.hip): the
     # lower / upper 128 of the flip of two sorted halves are bitonic; only
     # ranks 51..127 of the lower and 0..76 of the upper (global 128..204) are
@@ -120,7 +162,7 @@ def network_specs():
 
 def emit():
     lines = ["// GENERATED by gen_networks.py -- do not edit.",
-             "// Batcher odd-even merge sort networks over keys of type T (uint32 total-order",
+             "// Sorting networks (60-comparator 16-sorters + Batcher odd-even merges) over keys of type T (uint32 total-order",
              "// keys, or floats where min/max give the same order),",
              "// pruned to the wanted output ranks.  Counts are per coordinate.",
              "// P2P_CE / P2P_MIN / P2P_MAX are defined by the includer in terms of ASC.",

@@ -104,4 +104,21 @@ __device__ __forceinline__ bool all_aligned16(const float* const* peers, int K, 
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// One block per tile over a 2-D grid.  An AQL dispatch counts work-items in
+// 32 bits per dimension: one 128-lane block per 64 or 128 coordinates in x
+// alone would wrap past 2^31 / 2^32 coordinates and leave the rest of the
+// buffer untouched.  Tile t = blockIdx.y * gx + blockIdx.x with gx <= 2^24
+// blocks; the surplus blocks of the last row exit at once.
+constexpr int64_t kMaxGridX = int64_t(1) << 24;
+struct TileGrid {
+  unsigned gx, gy;
+};
+__host__ inline TileGrid tile_grid(int64_t tiles) {
+  const int64_t gx = tiles < kMaxGridX ? tiles : kMaxGridX;
+  return TileGrid{static_cast<unsigned>(gx), static_cast<unsigned>(gx > 0 ? ceil_div(tiles, gx) : 0)};
+}
+__device__ __forceinline__ int64_t tile_id(unsigned gx) {
+  return static_cast<int64_t>(__builtin_amdgcn_workgroup_id_y()) * gx + __builtin_amdgcn_workgroup_id_x();
+}
+
 }  // namespace p2p

@@ -180,17 +180,21 @@ __device__ __forceinline__ void robust_one(const float* const* peers, int K, int
   if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
 }
 
+// 2-D grid (p2p_common.h tile_grid): tile t = blockIdx.y * gx + blockIdx.x.
 template <int KP, int RULE, int MODE>
 __global__ __launch_bounds__(kRobustTile, MODE != 0 ? 3 : 1) void robust_flat_kernel(
     const float* const* __restrict__ peers, int K, int trim_b, int64_t n, float* w, float* out,
-    float lr) {
-  robust_one<KP, RULE, MODE>(peers, K, trim_b, n, bid_x(), w, out, lr);
+    float lr, int64_t ntiles, unsigned gx) {
+  const int64_t t = tile_id(gx);
+  if (t >= ntiles) return;
+  robust_one<KP, RULE, MODE>(peers, K, trim_b, n, t, w, out, lr);
 }
 
 template <int KP, int RULE, int MODE>
 __global__ __launch_bounds__(kRobustTile, MODE != 0 ? 3 : 1) void robust_segments_kernel(
-    const Seg* __restrict__ segs, int nseg, int K, int trim_b, float lr) {
-  const int64_t t = bid_x();
+    const Seg* __restrict__ segs, int nseg, int K, int trim_b, float lr, int64_t ntiles, unsigned gx) {
+  const int64_t t = tile_id(gx);
+  if (t >= ntiles) return;
   const Seg s = load_segment(segs, nseg, t);
   robust_one<KP, RULE, MODE>(s.peers, K, trim_b, s.n, t - s.tile_begin, s.w, s.out, lr);
 }
@@ -210,13 +214,15 @@ struct RobustArgs {
 
 template <int KP, int RULE, int MODE>
 static void launch_one(const RobustArgs& a) {
+  const int64_t tiles = a.segs ? a.tiles : ceil_div(a.n, kRobustTile);
+  const TileGrid g = tile_grid(tiles);
+  if (g.gx == 0) return;
   if (a.segs) {
-    hipLaunchKernelGGL((robust_segments_kernel<KP, RULE, MODE>), dim3(static_cast<unsigned>(a.tiles)),
-                       dim3(kRobustTile), 0, a.stream, a.segs, a.nseg, a.K, a.trim_b, a.lr);
+    hipLaunchKernelGGL((robust_segments_kernel<KP, RULE, MODE>), dim3(g.gx, g.gy), dim3(kRobustTile), 0, a.stream,
+                       a.segs, a.nseg, a.K, a.trim_b, a.lr, tiles, g.gx);
   } else {
-    hipLaunchKernelGGL((robust_flat_kernel<KP, RULE, MODE>),
-                       dim3(static_cast<unsigned>(ceil_div(a.n, kRobustTile))), dim3(kRobustTile), 0,
-                       a.stream, a.peers, a.K, a.trim_b, a.n, a.w, a.out, a.lr);
+    hipLaunchKernelGGL((robust_flat_kernel<KP, RULE, MODE>), dim3(g.gx, g.gy), dim3(kRobustTile), 0, a.stream,
+                       a.peers, a.K, a.trim_b, a.n, a.w, a.out, a.lr, tiles, g.gx);
   }
 }
 

@@ -324,10 +324,9 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
 template <int RULE, bool SEGS, bool SMALL>
 __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers, const Seg* __restrict__ segs,
                                           int nseg, int64_t n, float* w, float* out, float lr, Img im,
-                                          int __attribute__((address_space(3)))* flags) {
+                                          int __attribute__((address_space(3)))* flags, int64_t t) {
   const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
   const int lane = tid_x() & 63;
-  const int64_t t = bid_x();
   const float* const* P = peers;
   float* W = w;
   float* O = out;
@@ -362,11 +361,13 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
 template <bool SEGS, bool SMALL = false>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(
     const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n, float* w,
-    float* out, float lr) {
+    float* out, float lr, int64_t ntiles, unsigned gx) {
   __shared__ u32x4 img_raw[kHalf / 4 * 64 + 16];
   __shared__ int nan_flag[2];
+  const int64_t t = tile_id(gx);
+  if (t >= ntiles) return;  // block-uniform
   pair_tile<P2P_RULE_TRIMMED, SEGS, SMALL>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
-                                           (int __attribute__((address_space(3)))*)nan_flag);
+                                           (int __attribute__((address_space(3)))*)nan_flag, t);
 }
 
 // Median: 16 KB image (B's kept half) + both max(lo) (512 B), 3 waves per
@@ -374,33 +375,39 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
 template <bool SEGS, bool SMALL = false>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void robust_median_pair_kernel(
     const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n, float* w,
-    float* out, float lr) {
+    float* out, float lr, int64_t ntiles, unsigned gx) {
   __shared__ u32x4 img_raw[kHalf / 8 * 64 + 32];
   __shared__ int nan_flag[2];
+  const int64_t t = tile_id(gx);
+  if (t >= ntiles) return;  // block-uniform
   pair_tile<P2P_RULE_MEDIAN, SEGS, SMALL>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
-                                          (int __attribute__((address_space(3)))*)nan_flag);
+                                          (int __attribute__((address_space(3)))*)nan_flag, t);
 }
 
 }  // namespace p2p
 
 using namespace p2p;
 
-// K = 256, median or trimmed with b = 51: grid = one block per 64-coordinate
-// tile (flat: ceil(n / 64); segment table: `tiles`, tile_begin in units of 64).
+// K = 256, median or trimmed with b = 51: one block per 64-coordinate tile
+// (flat: ceil(n / 64); segment table: `tiles`, tile_begin in units of 64), on
+// a 2-D grid beyond 2^24 tiles.
 extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, const p2p_segment_t* segs,
                                                     int32_t nseg, int64_t tiles, int32_t rule, int64_t n,
                                                     float* w, float* out, float lr, p2p_stream_t stream) {
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  const int64_t grid = segs ? tiles : ceil_div(n, kPairTile);
-  if (grid <= 0) return;
-  const dim3 g(static_cast<unsigned>(grid)), b(2 * 64);
+  const int64_t ntiles = segs ? tiles : ceil_div(n, kPairTile);
+  const TileGrid tg = tile_grid(ntiles);  // 2 x 64 lanes per 64 coordinates: 1-D, n > 2^31 would wrap
+  if (tg.gx == 0) return;
+  const dim3 g(tg.gx, tg.gy), b(2 * 64);
+#define P2P_PAIR_ARGS g, b, 0, st, peers, segs, nseg, n, w, out, lr, ntiles, tg.gx
   if (rule == P2P_RULE_MEDIAN) {
-    if (segs) hipLaunchKernelGGL((robust_median_pair_kernel<true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_median_pair_kernel<false, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else hipLaunchKernelGGL((robust_median_pair_kernel<false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    if (segs) hipLaunchKernelGGL((robust_median_pair_kernel<true>), P2P_PAIR_ARGS);
+    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_median_pair_kernel<false, true>), P2P_PAIR_ARGS);
+    else hipLaunchKernelGGL((robust_median_pair_kernel<false>), P2P_PAIR_ARGS);
   } else {
-    if (segs) hipLaunchKernelGGL((robust_pair_kernel<true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_pair_kernel<false, true>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
-    else hipLaunchKernelGGL((robust_pair_kernel<false>), g, b, 0, st, peers, segs, nseg, n, w, out, lr);
+    if (segs) hipLaunchKernelGGL((robust_pair_kernel<true>), P2P_PAIR_ARGS);
+    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_pair_kernel<false, true>), P2P_PAIR_ARGS);
+    else hipLaunchKernelGGL((robust_pair_kernel<false>), P2P_PAIR_ARGS);
   }
+#undef P2P_PAIR_ARGS
 }

@@ -261,7 +261,7 @@ def test_dropin_plain_dicts_take_the_c_gather(cuda, monkeypatch):
         assert_bits_equal(got, want2, what="C gather round 2")
     assert len(calls) == 2
     missing = [dict(u) for u in upd]
-    del missing[3]["fc2.bias"]
+    del missing[3]["fc2__bias"]
     node = fake_node(model, missing)
     with pytest.raises(KeyError):
         agg.aggregate_models(node)
@@ -272,8 +272,8 @@ def test_dropin_plain_dicts_take_the_c_gather(cuda, monkeypatch):
     with torch.no_grad():
         model.load_state_dict(split(w0, shapes, cuda))
     odd = [dict(u) for u in upd]
-    odd[1]["fc1.weight"] = odd[1]["fc1.weight"].t().contiguous().t()
-    assert not odd[1]["fc1.weight"].is_contiguous()
+    odd[1]["fc1__weight"] = odd[1]["fc1__weight"].t().contiguous().t()
+    assert not odd[1]["fc1__weight"].is_contiguous()
     calls.clear()
     agg.aggregate_models(fake_node(model, odd))
     assert calls == []
@@ -531,6 +531,34 @@ def test_aggregate_beyond_2g_elements_sampled(cuda, rule):
     del peers, w
     torch.cuda.empty_cache()
     assert_bits_equal(got, want, what=f"{rule} n=2**31+37")
+
+
+@pytest.mark.parametrize("k", [256, 200])
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+@pytest.mark.parametrize("n", [(1 << 30) + 37, BIG_N])
+def test_robust_many_peers_beyond_2g_aliased_views(cuda, k, rule, n):
+    """the flat pair kernels' 64-bit instantiation (K = 256,
+    n > 2**30) and the 4-lane LDS kernels (K = 200) past 2**31 elements.  K
+    separate 8.6 GB peers do not fit 288 GB, so the peers are views of ONE
+    buffer shifted by 64 floats (256 B: DMA-aligned); sampled coordinates
+    (both ends, the 2**30 / 2**31 boundaries) against the oracle."""
+    shift, seed = 64, 0x5EED00B3
+    buf = torch.empty(n + (k - 1) * shift, dtype=torch.float32, device=cuda)
+    ops.fill_synthetic_(buf, seed, 0, 1e-2)  # element g = synth_at(g, seed, 0, .)
+    peers = [buf[p * shift:p * shift + n] for p in range(k)]
+    out = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate(peers, rule, out=out)
+    rng = np.random.default_rng(11)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 2000), np.arange(512), n - 1 - np.arange(512),
+                                    (1 << 30) - 3 + np.arange(8), (1 << 31) - 3 + np.arange(8)]))
+    idx = idx[idx < n]
+    got = out[torch.from_numpy(idx).to(cuda)].cpu().numpy()
+    del peers, buf, out
+    torch.cuda.empty_cache()
+    x = [oracle.synth_at(idx + p * shift, seed, 0, 1e-2) for p in range(k)]
+    r = ops.rule_id(rule)
+    _, want = oracle.robust(x, r, ops.trim_count(k) if r == 2 else 0)
+    assert_bits_equal(got, want, what=f"{rule} K={k} n={n} aliased")
 
 
 def test_delta_beyond_2g_elements_sampled(cuda):
