@@ -174,9 +174,16 @@ def emit():
         n1 = len(ops) - nce
         lines.append(f"// {tag}: KP={kp} wanted={'all' if wanted is None else f'{wanted[0]}..{wanted[-1]}'}"
                      f" comparators={nce} half-ops={n1} valu={2 * nce + n1}")
-        lines.append(f"template <bool ASC, typename T>  // ASC=false sorts descending (min/max swapped)")
-        lines.append(f"__device__ __forceinline__ void net_{tag}(T (&v)[{kp}]) {{")
+        lines.append(f"template <bool ASC, typename T, typename H = NoHook>  // ASC=false sorts descending")
+        lines.append(f"__device__ __forceinline__ void net_{tag}(T (&v)[{kp}], H&& hook = H{{}}) {{")
+        # hook(v, blk) runs before the first comparator that reads block blk
+        # (16 keys) -- the block still holds its inputs there.  A NaN test per
+        # block then waits only for that block's loads (robust_nets.h).
+        seen = set()
         for op, a, b in ops:
+            for blk in sorted({a // 16, b // 16} - seen) if kp >= 16 and base != "bmerge" else ():
+                lines.append(f"  hook(v, {blk});")
+                seen.add(blk)
             lines.append(f"  P2P_{op}(v[{a}], v[{b}]);")
         lines.append("}")
         lines.append("")

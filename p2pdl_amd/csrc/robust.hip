@@ -26,10 +26,12 @@ namespace p2p {
 
 constexpr int kRobustTile = 128;  // coordinates per block (one lane each)
 
-// K == KP, no NaN in the wave: the pruned rules on the float values (robust_nets.h:
-// same ranks and bits as the keys) -- no key map in (2 VALU per key) or out.
+// K == KP: the pruned rules on the float values (robust_nets.h: same ranks and
+// bits as the keys) -- no key map in (2 VALU per key) or out.  `nan` collects
+// the NaN test block by block as the networks first read each block; the
+// result is valid only when it stays 0.
 template <int KP, int RULE>
-__device__ __forceinline__ float special_floats(const uint32_t (&v)[KP]) {
+__device__ __forceinline__ float special_floats(const uint32_t (&v)[KP], uint64_t& nan) {
   if constexpr (RULE == P2P_RULE_MEDIAN) {
     constexpr int Q = KP / 4;
     fk a[Q], b[Q], c[Q], d[Q];
@@ -40,16 +42,16 @@ __device__ __forceinline__ float special_floats(const uint32_t (&v)[KP]) {
       c[j].x = __uint_as_float(v[2 * Q + j]);
       d[j].x = __uint_as_float(v[3 * Q + j]);
     }
-    sort_full<Q>(a);
-    sort_full<Q>(b);
-    sort_full<Q>(c);
-    sort_full<Q>(d);
+    sort_full<Q>(a, NanHook<>{nan});
+    sort_full<Q>(b, NanHook<>{nan});
+    sort_full<Q>(c, NanHook<>{nan});
+    sort_full<Q>(d, NanHook<>{nan});
     return four_list_median<Q>(a, b, c, d).x;
   } else {
     fx x[KP];
 #pragma unroll
     for (int j = 0; j < KP; ++j) x[j].x = __uint_as_float(v[j]);
-    run_special<KP, 2>(x);
+    run_special<KP, 2>(x, NanHook<>{nan});
     constexpr int b = (KP * 2) / 10;
     float acc = 0.f;
 #pragma unroll
@@ -86,7 +88,9 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
   }
   __builtin_amdgcn_sched_barrier(0);  // all KP loads in flight before the first use
   if constexpr (MODE != 0 && !KEYS) {  // K == KP: a NaN-free wave runs on the floats themselves
-    if (!__builtin_amdgcn_readfirstlane(static_cast<int>(wave_has_nan(v)))) return special_floats<KP, RULE>(v);
+    uint64_t nan = 0;
+    const float r = special_floats<KP, RULE>(v, nan);
+    if (!__builtin_amdgcn_readfirstlane(static_cast<int>(nan != 0))) return r;
     return robust_coord_keys<KP, RULE, MODE>(peers, K, trim_b, c0, lane_off);
   }
 #pragma unroll

@@ -154,6 +154,15 @@ __device__ __forceinline__ void pin(const T (&x)[N]) {
   for (int j = 0; j < N; ++j) asm volatile("" ::"v"(raw(x[j])));
 }
 
+// NaN test of N consecutive loaded keys (one v_cmp_u_f32 per two).
+template <int N>
+__device__ __forceinline__ uint64_t list_nan_mask(const uint32_t* v) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int j = 0; j < N / 2; ++j) m |= unordered_mask(__uint_as_float(v[j]), __uint_as_float(v[j + N / 2]));
+  return m;
+}
+
 // One half sorted in T's domain (the block's: keys if either half holds a
 // NaN); returns the aggregate, valid in wave 0.  Both waves pass the same
 // number of block barriers.
@@ -173,17 +182,22 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
 // image leaves room for 3 blocks' worth of waves per SIMD pair.
 template <typename T, bool FLAGS = false>
 __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im, int h, int lane,
-                                             int __attribute__((address_space(3)))* flags = nullptr, bool nan = false,
+                                             int __attribute__((address_space(3)))* flags = nullptr,
                                              const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0) {
   constexpr int Q = kHalf / 2;  // 64 keys per sorted list
+  // FLAGS: each list's NaN test right before its sort, so sorting p overlaps
+  // q's loads (a test of all 128 up front waited for every load: +3.5% time)
   T p[Q], q[Q];
+  uint64_t nan = 0;
+  if constexpr (FLAGS) nan = list_nan_mask<Q>(v);
 #pragma unroll
-  for (int j = 0; j < Q; ++j) {
-    p[j] = from_bits<T>(v[j]);
-    q[j] = from_bits<T>(v[Q + j]);
-  }
+  for (int j = 0; j < Q; ++j) p[j] = from_bits<T>(v[j]);
   sort_full<Q>(p);
+  if constexpr (FLAGS) nan |= list_nan_mask<Q>(v + Q);
+#pragma unroll
+  for (int j = 0; j < Q; ++j) q[j] = from_bits<T>(v[Q + j]);
   sort_full<Q>(q);
+  const bool has_nan = FLAGS && uniform(nan != 0);  // to a bool at once (a live mask spilled SGPRs)
   pin(p);
   pin(q);
   // max_j min(p_j, q_{63-j}) as a v_max3 chain (the mins consumed as made)
@@ -194,7 +208,7 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
   auto part = (uint32_t __attribute__((address_space(3)))*)(im + Q / 4 * 64);  // max(lo) of wave h at [64h + lane]
   part[h * 64 + lane] = raw(m);
   if constexpr (FLAGS) {
-    if (lane == 0) flags[h] = nan ? 1 : 0;
+    if (lane == 0) flags[h] = has_nan ? 1 : 0;
   }
   block_sync();  // 1: both max(lo)
   if constexpr (FLAGS) {
@@ -224,12 +238,22 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
 // network (pair_keys) -- the float sort of a NaN half is discarded.
 template <int RULE, typename T, bool FLAGS = false>
 __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, int h, int lane,
-                                           int __attribute__((address_space(3)))* flags = nullptr, bool nan = false,
+                                           int __attribute__((address_space(3)))* flags = nullptr,
                                            const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0) {
   T x[kHalf];
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) x[j] = from_bits<T>(v[j]);
-  sort_full<kHalf>(x);
+  // FLAGS: the first half's NaN test before the sort, the second half's when
+  // the sort first reads it (NanHook at block 4), so the sort of the first 64
+  // overlaps the last loads
+  uint64_t nan = 0;
+  if constexpr (FLAGS) {
+    nan = list_nan_mask<kHalf / 2>(v);
+    sort_full<kHalf>(x, NanHook<4, 4>{nan});
+  } else {
+    sort_full<kHalf>(x);
+  }
+  const bool has_nan = FLAGS && uniform(nan != 0);
   pin(x);
   {
     // each wave hands over its upper 64 (groups 16..31) into its own half of
@@ -241,7 +265,7 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
           u32x4{raw(x[4 * g]), raw(x[4 * g + 1]), raw(x[4 * g + 2]), raw(x[4 * g + 3])};
   }
   if constexpr (FLAGS) {
-    if (lane == 0) flags[h] = nan ? 1 : 0;
+    if (lane == 0) flags[h] = has_nan ? 1 : 0;
   }
   block_sync();  // 1: A in the image
   if constexpr (FLAGS) {
@@ -347,10 +371,9 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
   load_half(v, P, cb, lane_off, h);
   // One domain per block: the float network unless either half holds a NaN
   // (flags swapped at the first barrier, no barrier of their own).
-  const bool nan = uniform(wave_has_nan(v));
   float agg;
-  if constexpr (RULE == P2P_RULE_MEDIAN) agg = median_pair<fk, true>(v, im, h, lane, flags, nan, P, cb, lane_off);
-  else agg = pair_body<RULE, fk, true>(v, im, h, lane, flags, nan, P, cb, lane_off);
+  if constexpr (RULE == P2P_RULE_MEDIAN) agg = median_pair<fk, true>(v, im, h, lane, flags, P, cb, lane_off);
+  else agg = pair_body<RULE, fk, true>(v, im, h, lane, flags, P, cb, lane_off);
   if (h == 0 && i < N) {  // wave 0 holds the aggregate
     if (O) stg(O + i, agg);
     if (W) stg(W + i, apply_lr(ldg(W + i), lr, agg));
