@@ -137,3 +137,43 @@ def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor],
     if comm is not None:
         comp.wait_stream(comm)
     return plan
+
+
+# ------------------------------------------------------------------ digests
+def sharded_digests(messages: Sequence[bytes], *, group=None, digest: Callable | None = None,
+                    device=None) -> list:
+    """SHA-256 of K serialized updates sharded BY PEER over the ranks of a
+    group (digest row; reference utils/crypto.py:54-57 hashes
+    each update inside ECDSA(SHA256())).  Message j belongs to rank j % G; each
+    rank hashes its own with the GPU batch kernel (K3, ``ops.sha256_batch``)
+    and one all-gather of 32 B per message (RCCL for an ``nccl`` group, the
+    group's own backend otherwise) gives every rank all K digests in list
+    order.  ``digest`` (bytes list -> 32-byte digests) is a test seam.
+
+    Every chain advances at one lane's issue rate, so the aggregate rate is
+    the number of chains times that rate on 1 or G GPUs alike (DESIGN.md §3
+    K3); sharding spreads the host-to-device copies and the lanes, it does
+    not shorten the longest chain."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    k = len(messages)
+    mine = list(messages[rank::world])
+    if digest is None:
+        from . import ops
+
+        out = ops.sha256_batch(mine, device=device) if mine else []
+    else:
+        out = list(digest(mine)) if mine else []
+    if world == 1:
+        return out
+    per = -(-k // world)  # messages per rank, padded
+    on_gpu = dist.get_backend(group) == "nccl"
+    dev = (device or torch.device("cuda", torch.cuda.current_device())) if on_gpu else torch.device("cpu")
+    local = torch.zeros((per, 32), dtype=torch.uint8)
+    for i, d in enumerate(out):
+        local[i] = torch.frombuffer(bytearray(d), dtype=torch.uint8)
+    local = local.to(dev)
+    parts = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(parts, local, group=group)
+    parts = [p.cpu().numpy() for p in parts]
+    return [bytes(parts[j % world][j // world]) for j in range(k)]
