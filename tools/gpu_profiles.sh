@@ -4,7 +4,7 @@
 #     record's kernel, the numbers bench.py's HIP events must agree with);
 #   * HBM traffic per launch for every bench record (FETCH_SIZE and
 #     WRITE_SIZE in separate passes, tools/pmc_traffic.py -> traffic_*.json);
-#   * SQ / GRBM counters of the K = 256 robust kernels.
+#   * SQ / GRBM counters of the robust kernels (K = 256 and cfg4).
 # Each GPU step has its own time limit; the chain stops at the first failure.
 #   usage: tools/gpu_profiles.sh <out-dir under gpurun_out/>
 set -o pipefail
@@ -40,12 +40,13 @@ cfg3-chunk:fedavg_flat_kernel:15625000:256:--job cfg3-full --steps 1
 cfg2-dropin:fedavg_segments_kernel:11689512:64:--workload cfg2-dropin
 cfg4-median:robust_flat_kernel:100000000:128:--workload cfg4-median
 cfg4-trimmed:robust_flat_kernel:100000000:128:--workload cfg4-trimmed
-median256:robust_pair_kernel:100000000:256:--workload median256
+median256:robust_median_pair_kernel:100000000:256:--workload median256
 trimmed256:robust_pair_kernel:100000000:256:--workload trimmed256
+delta:delta_flat_kernel:1000000000:1:--workload delta
 EOS
 
 # issue / wait / clock counters of the K = 256 robust kernels (8 SQ + 2 GRBM slots)
-for w in median256 trimmed256; do
+for w in median256 trimmed256 cfg4-median cfg4-trimmed; do
   run 240 "$OUT/pmc_sq_$w.log" timeout -s KILL 220 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT $F -d "$OUT/pmc_sq_$w" -o run -- python3 -u $B --workload $w
 done
 ls "$OUT"
