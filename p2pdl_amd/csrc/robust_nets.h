@@ -102,6 +102,45 @@ struct NanHook {
     for (int j = 0; j < N / 2; ++j) m |= unordered_mask(bits_f(v[16 * blk + j]), bits_f(v[16 * blk + N / 2 + j]));
   }
 };
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  return max(min(a, b), min(max(a, b), c));  // -> v_med3_u32
+}
+
+// The generated networks' instructions (gen_networks.py lowers every
+// comparator network to one of these per computed value).  ASC = false is the
+// mirror image: min <-> max, med3 unchanged.  Three-input forms become
+// v_min3 / v_max3 / v_med3 (f32 for fk / fx, u32 for keys).
+template <bool ASC, typename T>
+__device__ __forceinline__ T lo2(T a, T b) { return ASC ? min(a, b) : max(a, b); }
+template <bool ASC, typename T>
+__device__ __forceinline__ T hi2(T a, T b) { return ASC ? max(a, b) : min(a, b); }
+// The other output of a comparator whose `lo` is computed too: plain max for
+// fk / uint32_t; a ^ b ^ lo (one v_bitop3) for kx / fx, which keeps fewer
+// values live (see kx above).
+template <bool ASC, typename T>
+__device__ __forceinline__ T hi_sib(T a, T b, T) { return hi2<ASC>(a, b); }
+template <bool ASC>
+__device__ __forceinline__ kx hi_sib(kx a, kx b, kx lo) { return kx{static_cast<uint32_t>(__builtin_amdgcn_bitop3_b32(a.k, b.k, lo.k, 0x96))}; }
+template <bool ASC>
+__device__ __forceinline__ fx hi_sib(fx a, fx b, fx lo) {
+  return fx{__uint_as_float(
+      __builtin_amdgcn_bitop3_b32(__float_as_uint(a.x), __float_as_uint(b.x), __float_as_uint(lo.x), 0x96))};
+}
+template <bool ASC, typename T>
+__device__ __forceinline__ T lo3(T a, T b, T c) { return lo2<ASC>(lo2<ASC>(a, b), c); }
+template <bool ASC, typename T>
+__device__ __forceinline__ T hi3(T a, T b, T c) { return hi2<ASC>(hi2<ASC>(a, b), c); }
+__device__ __forceinline__ uint32_t med3(uint32_t a, uint32_t b, uint32_t c) { return umed3(a, b, c); }
+__device__ __forceinline__ kx med3(kx a, kx b, kx c) { return kx{umed3(a.k, b.k, c.k)}; }
+__device__ __forceinline__ fk med3(fk a, fk b, fk c) { return fk{__builtin_amdgcn_fmed3f(a.x, b.x, c.x)}; }
+__device__ __forceinline__ fx med3(fx a, fx b, fx c) { return fx{__builtin_amdgcn_fmed3f(a.x, b.x, c.x)}; }
+#define P2P_LO(a, b) lo2<ASC>((a), (b))
+#define P2P_HI(a, b) hi2<ASC>((a), (b))
+#define P2P_HIS(a, b, lo) hi_sib<ASC>((a), (b), (lo))
+#define P2P_LO3(a, b, c) lo3<ASC>((a), (b), (c))
+#define P2P_HI3(a, b, c) hi3<ASC>((a), (b), (c))
+#define P2P_MED3(a, b, c) med3((a), (b), (c))
+// the round-2 two-input form (gen_networks.py --classic, A/B builds)
 #define P2P_CE(a, b) ce<ASC>((a), (b))
 #define P2P_MIN(a, b) (a) = (ASC ? min((a), (b)) : max((a), (b)))
 #define P2P_MAX(a, b) (b) = (ASC ? max((a), (b)) : min((a), (b)))
@@ -109,13 +148,16 @@ struct NanHook {
 #undef P2P_CE
 #undef P2P_MIN
 #undef P2P_MAX
+#undef P2P_LO
+#undef P2P_HI
+#undef P2P_HIS
+#undef P2P_LO3
+#undef P2P_HI3
+#undef P2P_MED3
 
 // keep(a, b, lim): min(a, b) when lim is the bottom of the order, max(a, b)
 // when it is the top -- ONE v_med3 against a lane-constant 0 / ~0 (keys) or
 // -inf / +inf (floats; v_med3_f32 orders -0 < +0, tools/fminmax_probe.hip).
-__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
-  return max(min(a, b), min(max(a, b), c));  // -> v_med3_u32
-}
 __device__ __forceinline__ uint32_t keep(uint32_t a, uint32_t p, uint32_t lim) { return umed3(a, p, lim); }
 __device__ __forceinline__ fk keep(fk a, fk p, fk lim) { return fk{__builtin_amdgcn_fmed3f(a.x, p.x, lim.x)}; }
 __device__ __forceinline__ uint32_t keep_limit(uint32_t, bool hi) { return hi ? 0xFFFFFFFFu : 0u; }
