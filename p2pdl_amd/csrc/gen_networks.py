@@ -2,12 +2,10 @@
 """Generate register-resident sorting / selection networks for the robust kernels.
 
 Each network sorts (or partially sorts) KP keys held in a fully unrolled
-register array.  The base network sorts blocks of 16 with a 60-comparator
-network and merges them with Batcher's odd-even merges (1447 comparators for
-128 against 1471 for Batcher's odd-even merge sort).  For a fixed set of wanted
-output ranks the network is pruned backwards: a comparator whose two outputs
-are both dead is dropped, one with a single live output becomes a lone min or
-max.
+register array: Batcher's odd-even merge sort, or a bitonic merger for the
+flip of two sorted lists.  For a fixed set of wanted output ranks the network
+is pruned backwards: a comparator whose two outputs are both dead is dropped,
+one with a single live output becomes a lone min or max.
 
 Three-input lowering (round 3).  A comparator network issues one VALU
 instruction per comparator output.  gfx950 has full-rate three-input
@@ -26,8 +24,9 @@ all inputs.  Pruned networks are checked on the same domains -- every live
 value is computed exactly as in the unpruned network.  A greedy pass from the
 outputs backwards eliminates a node when all its consumers can absorb it (each
 consumer absorbs at most one operand, and an eliminated node's operands must
-themselves be computed).  sort128: 2894 -> 2248 VALU, bmerge128 pruned to
-ranks 51..127: 619 -> 430.
+themselves be computed); an exact MILP of the same selection problem finds
+at most 0.7% more.  sort128: 2942 -> 2184 VALU (round 2's 16-block network:
+2894), bmerge128 pruned to ranks 51..127: 619 -> 430.
 
 Output: networks.inc (committed; regenerate with `python gen_networks.py`;
 `--classic` writes the round-2 two-input form, for A/B builds only).
@@ -108,6 +107,19 @@ def green_batcher(n: int, lo: int = 0):
             + [(c, ("merge", lo, n)) for c in oddeven_merge(lo, lo + n - 1, 1)])
 
 
+def batcher_stages(n: int, lo: int = 0):
+    """Batcher's odd-even merge sort of [lo, lo + n), each merge its own
+    stage (two sorted halves in).  More comparators than green_batcher's
+    16-blocks (1471 against 1447 for 128) but fewer instructions once
+    lowered to three-input forms (2184 against 2248): the 16-sorter's
+    irregular layers leave fewer minima / maxima for a consumer to absorb."""
+    if n == 1:
+        return []
+    h = n // 2
+    return (batcher_stages(h, lo) + batcher_stages(h, lo + h)
+            + [(c, ("merge", lo, n)) for c in oddeven_merge(lo, lo + n - 1, 1)])
+
+
 def bitonic_merge(n: int):
     """Comparators sorting a BITONIC sequence of n (power of 2) ascending:
     half-cleaners at distance n/2, n/4, ..., 1."""
@@ -121,7 +133,10 @@ def bitonic_merge(n: int):
     return comps
 
 
-NETWORKS = {"bmerge": bitonic_merge, "green": green_batcher}
+# base network per emission form: "sort" is Batcher's merge sort when lowered
+# to three-input forms, the 16-block network in the round-2 (--classic) form
+NETWORKS = {"bmerge": bitonic_merge, "sort": batcher_stages}
+CLASSIC = {"bmerge": bitonic_merge, "sort": green_batcher}
 
 
 def domain(stage):
@@ -347,14 +362,14 @@ def network_specs():
     (robust_lds.hip, either direction, bmerge64 across lanes)."""
     specs = []
     for kp in (2, 4, 8, 16, 32, 64, 128):
-        specs.append((f"sort{kp}", kp, None, "green"))
+        specs.append((f"sort{kp}", kp, None, "sort"))
     for kp in (32, 64, 128):
         specs.append((f"bmerge{kp}", kp, None, "bmerge"))
     # specialised K == KP instances for the benchmark configurations
     for kp in (64, 128):
-        specs.append((f"median{kp}", kp, [(kp - 1) // 2], "green"))
+        specs.append((f"median{kp}", kp, [(kp - 1) // 2], "sort"))
         b = int(0.2 * kp + 1e-9)
-        specs.append((f"trim{kp}_b{b}", kp, list(range(b, kp - b)), "green"))
+        specs.append((f"trim{kp}_b{b}", kp, list(range(b, kp - b)), "sort"))
     # trimmed mean of 256 in one lane per coordinate (robust_pair.hip): the
     # lower / upper 128 of the flip of two sorted halves are bitonic; only
     # ranks 51..127 of the lower and 0..76 of the upper (global 128..204) are
@@ -373,7 +388,7 @@ def build(tag, kp, wanted, base):
 
 
 HEADER = ["// GENERATED by gen_networks.py -- do not edit.",
-          "// Sorting networks (60-comparator 16-sorters + Batcher odd-even merges, or bitonic mergers) over",
+          "// Sorting networks (Batcher odd-even merge sorts, or bitonic mergers) over",
           "// values of type T (uint32 total-order keys, or floats where min / max give the same order),",
           "// pruned to the wanted output ranks.  Counts are per coordinate."]
 
@@ -381,7 +396,7 @@ HEADER = ["// GENERATED by gen_networks.py -- do not edit.",
 def emit_classic():
     lines = HEADER + ["// P2P_CE / P2P_MIN / P2P_MAX are defined by the includer in terms of ASC.", "#pragma once", ""]
     for tag, kp, wanted, base in network_specs():
-        ops = prune(NETWORKS[base](kp), wanted if wanted is not None else range(kp))
+        ops = prune(CLASSIC[base](kp), wanted if wanted is not None else range(kp))
         nce = sum(1 for (o, _, _), _ in ops if o == "CE")
         n1 = len(ops) - nce
         lines.append(f"// {tag}: KP={kp} wanted={'all' if wanted is None else f'{wanted[0]}..{wanted[-1]}'}"

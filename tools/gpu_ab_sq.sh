@@ -35,7 +35,23 @@ done
 for f in "$OUT"/prod*.log "$OUT"/lib*.log; do
   [ -f "$f" ] && echo "$(basename $f .log) $(grep -h '"kernel_ms"' $f | sed 's/.*"frac": \([0-9.]*\).*"kernel_ms": \([0-9.]*\).*/frac=\1 kernel_ms=\2/')"
 done
+# counters with the kernel trace (durations -> effective clock), for the
+# product library and every alternative
+PMC="--kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
 for w in $WL; do
-  run 200 "$OUT/pmc_sq_$w.log" timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT -d "$OUT/pmc_sq_$w" -o run -- python3 -u $B --workload $w --steps 2
+  run 200 "$OUT/pmc_sq_$w.log" timeout -s KILL 180 rocprofv3 $PMC -d "$OUT/pmc_sq_$w" -o run -- python3 -u $B --workload $w --steps 2
+  python3 tools/rocpd_summary.py "$OUT/pmc_sq_$w" robust > "$OUT/sq_$w.json" || true
+  for a in ${ALT//:/ }; do
+    P2P_LIB=$a run 200 "$OUT/pmc_sq_$(basename $a .so)_$w.log" timeout -s KILL 180 rocprofv3 $PMC -d "$OUT/pmc_sq_$(basename $a .so)_$w" -o run -- python3 -u $B --workload $w --steps 2
+    python3 tools/rocpd_summary.py "$OUT/pmc_sq_$(basename $a .so)_$w" robust > "$OUT/sq_$(basename $a .so)_$w.json" || true
+  done
 done
+python3 - "$OUT" <<'PY' || true
+import glob, json, os, sys
+for f in sorted(glob.glob(os.path.join(sys.argv[1], "sq_*.json"))):
+    d = json.load(open(f))
+    for p in d.get("pmc", []):
+        print(os.path.basename(f), "valu/wave=%.1f" % p.get("valu_insts_per_wave", 0), "clock=%.3f GHz" % p.get("effective_clock_ghz", 0),
+              "kernel_us=%.1f" % ([k["avg_ns"] for k in d["kernels"] if k["name"] == p["kernel"]] or [0])[0] / 1e3)
+PY
 ls "$OUT"
