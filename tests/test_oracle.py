@@ -89,6 +89,17 @@ def test_sorting_networks_0_1_principle():
     gen_networks.check()
 
 
+def test_committed_networks_are_the_generated_ones():
+    """networks.inc (what the kernels compile) is exactly gen_networks.py's
+    checked output, three-input lowering included."""
+    csrc = os.path.join(os.path.dirname(os.path.dirname(__file__)), "p2pdl_amd", "csrc")
+    sys.path.insert(0, csrc)
+    import gen_networks
+
+    with open(os.path.join(csrc, "networks.inc")) as f:
+        assert f.read() == "\n".join(gen_networks.emit_fused())
+
+
 def test_delta_snapshot_oracle_matches_torch_reference_ops():
     """oracle.delta_snapshot_np == the reference's torch ops (node/node.py:275,279,282)."""
     import torch

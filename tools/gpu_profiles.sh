@@ -47,6 +47,7 @@ EOS
 
 # issue / wait / clock counters of the K = 256 robust kernels (8 SQ + 2 GRBM slots)
 for w in median256 trimmed256 cfg4-median cfg4-trimmed; do
-  run 240 "$OUT/pmc_sq_$w.log" timeout -s KILL 220 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT $F -d "$OUT/pmc_sq_$w" -o run -- python3 -u $B --workload $w
+  run 240 "$OUT/pmc_sq_$w.log" timeout -s KILL 220 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT $F -d "$OUT/pmc_sq_$w" -o run -- python3 -u $B --workload $w
+  python3 tools/rocpd_summary.py "$OUT/pmc_sq_$w" robust > "$OUT/sq_$w.json" || true
 done
 ls "$OUT"
