@@ -135,8 +135,13 @@ def bitonic_merge(n: int):
 
 # base network per emission form: "sort" is Batcher's merge sort when lowered
 # to three-input forms, the 16-block network in the round-2 (--classic) form
-NETWORKS = {"bmerge": bitonic_merge, "sort": batcher_stages}
-CLASSIC = {"bmerge": bitonic_merge, "sort": green_batcher}
+def merge_stage(n: int):
+    """Batcher's odd-even merge of the two sorted halves of n keys."""
+    return [(c, ("merge", 0, n)) for c in oddeven_merge(0, n - 1, 1)]
+
+
+NETWORKS = {"bmerge": bitonic_merge, "sort": batcher_stages, "merge": merge_stage}
+CLASSIC = {"bmerge": bitonic_merge, "sort": green_batcher, "merge": merge_stage}
 
 
 def domain(stage):
@@ -370,12 +375,13 @@ def network_specs():
         specs.append((f"median{kp}", kp, [(kp - 1) // 2], "sort"))
         b = int(0.2 * kp + 1e-9)
         specs.append((f"trim{kp}_b{b}", kp, list(range(b, kp - b)), "sort"))
-    # trimmed mean of 256 in one lane per coordinate (robust_pair.hip): the
-    # lower / upper 128 of the flip of two sorted halves are bitonic; only
-    # ranks 51..127 of the lower and 0..76 of the upper (global 128..204) are
-    # summed, so each merger is pruned to those ranks.
-    specs.append(("bmerge128_r51_127", 128, list(range(51, 128)), "bmerge"))
-    specs.append(("bmerge128_r0_76", 128, list(range(0, 77)), "bmerge"))
+    # trimmed mean of 256 (robust_pair.hip): Batcher's odd-even merge of the
+    # two waves' sorted 128 split by parity -- v = merge(A_even, B_even) in
+    # wave 0, w = merge(A_odd, B_odd) in wave 1; ranks 51..204 of the merge
+    # need v_26..v_102 and w_25..w_101.  (bmerge128: the flip variant's
+    # mergers, for the 4-lane LDS kernels' cross-lane form.)
+    specs.append(("merge128_r26_102", 128, list(range(26, 103)), "merge"))
+    specs.append(("merge128_r25_101", 128, list(range(25, 102)), "merge"))
     return specs
 
 
@@ -405,7 +411,7 @@ def emit_classic():
         lines.append(f"__device__ __forceinline__ void net_{tag}(T (&v)[{kp}], H&& hook = H{{}}) {{")
         seen = set()
         for (op, a, b), _ in ops:
-            for blk in sorted({a // 16, b // 16} - seen) if kp >= 16 and base != "bmerge" else ():
+            for blk in sorted({a // 16, b // 16} - seen) if kp >= 16 and base == "sort" else ():
                 lines.append(f"  hook(v, {blk});")
                 seen.add(blk)
             lines.append(f"  P2P_{op}(v[{a}], v[{b}]);")
@@ -439,7 +445,7 @@ def emit_fused():
             # hook(v, blk) runs before the first instruction that reads input
             # block blk (16 keys) -- v still holds the inputs there
             blks = {x // 16 for x in a if x is not None and x < kp}
-            for blk in sorted(blks - seen) if kp >= 16 and base != "bmerge" else ():
+            for blk in sorted(blks - seen) if kp >= 16 and base == "sort" else ():
                 lines.append(f"  hook(v, {blk});")
                 seen.add(blk)
             if op == "lo":
@@ -474,6 +480,12 @@ def check():
                     s = np.concatenate([np.sort(x[r, :h[r]]), np.sort(x[r, h[r]:])[::-1]])
                     x[r] = np.roll(s, int(rng.integers(kp)))
                 rows.append(x)
+            inputs = np.concatenate(rows)
+        elif base == "merge":  # every 0-1 pair of sorted halves, and sorted halves of random values
+            rows = [np.array(domain(("merge", 0, kp)), dtype=np.uint64)]
+            for m in (3, 1 << 32):
+                x = rng.integers(0, m, size=(3000, kp), dtype=np.uint64)
+                rows.append(np.concatenate([np.sort(x[:, :kp // 2], axis=1), np.sort(x[:, kp // 2:], axis=1)], axis=1))
             inputs = np.concatenate(rows)
         elif kp <= 16:
             m = np.arange(1 << kp, dtype=np.uint64)

@@ -7,21 +7,20 @@
 // then w += lr*agg, multiply and add separately rounded (aggregation.py:36-38).
 //
 // Wave h loads peers 128h..128h+127 of its 64 coordinates (every load
-// instruction reads 256 contiguous bytes of one peer) and sorts them in
-// VGPRs with Batcher's 128-key network -- half A (h = 0) and half B (h = 1).
-// The two sorted halves meet in one flip:
-//   L_j = min(B_j, A_{127-j}),  U_j = max(B_j, A_{127-j})   (j = 0..127)
-// L is the 128 smallest keys of the coordinate, U the 128 largest, each a
-// bitonic sequence.  Each wave hands its upper 64 keys to the other through
-// LDS (16 KB each, one ds_write_b128 per 4 keys) and takes half of the pairs:
-// wave 1 (B_j, A_{127-j}) for j < 64, wave 0 (A_i, B_{127-i}) for i < 64.
-//   median : rank 127 = max_j L_j -- each wave a partial max over its 64
-//            pairs (64 v_min, 32 v_max3), wave 0's crosses LDS; no merge.
-//   trimmed: wave 1 keeps L, wave 0 keeps U, the missing quarters cross LDS;
-//            wave 1 merges L pruned to ranks 51..127, wave 0 merges U pruned
-//            to ranks 0..76, and the ascending sum runs over L's ranks in
-//            wave 1 and carries on over U's in wave 0 (the partial crosses
-//            LDS through a slot of its own).
+// instruction reads 256 contiguous bytes of one peer) -- half A (h = 0) and
+// half B (h = 1).
+//   median : each wave sorts its half as two lists of 64 and the two-set
+//            search (robust_nets.h) finds rank 127 without merging them.
+//   trimmed: each wave sorts its 128 (Batcher, three-input lowered) and the
+//            two halves meet in Batcher's odd-even merge split by parity:
+//            v = merge(A_even, B_even) in wave 0, w = merge(A_odd, B_odd) in
+//            wave 1 (each hands the other parity over, 16 KB), pruned to the
+//            ranks that reach 51..204 (398 instructions each); the merged
+//            order is c_{2i-1} = min(v_i, w_{i-1}), c_{2i} = max(v_i, w_{i-1}),
+//            so 39 values cross per wave, wave 1 sums c_51..c_127 ascending
+//            and wave 0 carries on over c_128..c_204 (the partial crosses LDS
+//            through a slot of its own).  Against the round-2 flip + pruned
+//            bitonic mergers: 475 instead of 558 instructions per wave.
 // Against the 4-lanes-per-coordinate LDS kernel this issues ~10% (median) /
 // ~22% (trimmed) fewer VALU instructions per coordinate -- two 128-key sorts
 // instead of four 64-key sorts plus cross-lane bitonic merges, no DPP moves,
@@ -47,29 +46,21 @@ __device__ __forceinline__ float val(fk x) { return x.x; }
 __device__ __forceinline__ uint32_t raw(fk x) { return __float_as_uint(x.x); }
 __device__ __forceinline__ uint32_t raw(uint32_t k) { return k; }
 __device__ __forceinline__ float val(uint32_t k) { return __uint_as_float(key2f(k)); }
+__device__ __forceinline__ uint32_t raw(kx k) { return k.k; }
+__device__ __forceinline__ float val(kx k) { return __uint_as_float(key2f(k.k)); }
 template <typename T> __device__ __forceinline__ T from_bits(uint32_t b);
 template <> __device__ __forceinline__ fk from_bits<fk>(uint32_t b) { return fk{__uint_as_float(b)}; }
 template <> __device__ __forceinline__ uint32_t from_bits<uint32_t>(uint32_t b) { return f2key(b); }
+template <> __device__ __forceinline__ kx from_bits<kx>(uint32_t b) { return kx{f2key(b)}; }
 // An element as it crosses LDS: the T-domain word itself (float bits or key).
 template <typename T> __device__ __forceinline__ T from_raw(uint32_t b);
 template <> __device__ __forceinline__ fk from_raw<fk>(uint32_t b) { return fk{__uint_as_float(b)}; }
 template <> __device__ __forceinline__ uint32_t from_raw<uint32_t>(uint32_t b) { return b; }
+template <> __device__ __forceinline__ kx from_raw<kx>(uint32_t b) { return kx{b}; }
 
 // LDS image of one sorted half: element j of lane l at word (j & 3) of
 // slot [j >> 2][l] -- 1 KiB per ds_write_b128 / ds_read_b128, no bank conflict.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-// Image slots read ahead of their use: the compiler would otherwise issue all
-// 32 reads at once (and hold the other half in 128 more VGPRs).  fence_after
-// makes a result computed from the slots read so far an input of a
-// memory-clobbering asm, so neither that arithmetic sinks below nor later
-// reads rise above it.
-constexpr int kReadAhead = 4;
-template <typename T>
-__device__ __forceinline__ void fence_after(T& x) {
-  uint32_t r = raw(x);
-  asm volatile("" : "+v"(r)::"memory");
-  x = from_raw<T>(r);
-}
 using Img = u32x4 __attribute__((address_space(3)))*;
 
 __device__ __forceinline__ uint32_t img_at(Img im, int j, int lane) { return im[(j >> 2) * 64 + lane][j & 3]; }
@@ -89,54 +80,16 @@ __device__ __forceinline__ void store_half(Img im, const T (&x)[kHalf], int lane
     im[g * 64 + lane] = u32x4{raw(x[4 * g]), raw(x[4 * g + 1]), raw(x[4 * g + 2]), raw(x[4 * g + 3])};
 }
 
-// trimmed, split flip: this wave's half X against the other's upper half Y
-// (in `other`): for i < 64, lo/hi of (X_i, Y_{127-i}); KEEP_LO keeps lo at
-// X_i and parks hi at X_{64+i} (the upper half, already handed over), else
-// the reverse.
-template <bool KEEP_LO, typename T>
-__device__ __forceinline__ void flip_half(Img other, T (&x)[kHalf], int lane) {
-  constexpr int Q = kHalf / 2;
+// m[FIRST .. FIRST+N-1] as elements 0..N-1 of an image region.
+template <int FIRST, int N, typename T>
+__device__ __forceinline__ void send_run(Img dst, const T (&m)[kHalf], int lane) {
 #pragma unroll
-  for (int g = 0; g < Q / 4; ++g) {
-    const u32x4 y4 = other[(Q / 4 - 1 - g) * 64 + lane];  // Y_{127-4g-k} = word 3-k
+  for (int g = 0; g < (N + 3) / 4; ++g) {
+    u32x4 q;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const T y = from_raw<T>(y4[3 - k]);
-      const T lo = min(x[4 * g + k], y), hi = max(x[4 * g + k], y);
-      x[4 * g + k] = KEEP_LO ? lo : hi;
-      x[Q + 4 * g + k] = KEEP_LO ? hi : lo;
-    }
-    if (g % kReadAhead == kReadAhead - 1) fence_after(x[4 * g + 3]);
+    for (int k = 0; k < 4; ++k) q[k] = 4 * g + k < N ? raw(m[FIRST + 4 * g + k]) : 0u;
+    dst[g * 64 + lane] = q;
   }
-}
-
-// trimmed, wave 1: L_j = min(B_j, A_{127-j}) stays in b; U_j = max(...) is
-// written over A_{127-j}'s word (each slot is read before it is rewritten).
-template <typename T>
-__device__ __forceinline__ void flip_write_upper(Img im, T (&b)[kHalf], int lane) {
-#pragma unroll
-  for (int g = 0; g < kHalf / 4; ++g) {
-    const int s = (kHalf / 4 - 1 - g) * 64 + lane;
-    const u32x4 a4 = im[s];
-    u32x4 u;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const T a = from_raw<T>(a4[3 - k]);
-      const T lo = min(b[4 * g + k], a), hi = max(b[4 * g + k], a);
-      b[4 * g + k] = lo;
-      u[3 - k] = raw(hi);
-    }
-    im[s] = u;
-    if (g % kReadAhead == kReadAhead - 1) fence_after(b[4 * g + 3]);
-  }
-}
-
-// Sum of ranks [R0, R1) of a merged half, ascending, continuing from acc.
-template <int R0, int R1, typename T>
-__device__ __forceinline__ float sum_ranks(const T (&x)[kHalf], float acc) {
-#pragma unroll
-  for (int j = R0; j < R1; ++j) acc = __fadd_rn(acc, val(x[j]));
-  return acc;
 }
 
 __device__ __forceinline__ void block_sync() {
@@ -255,57 +208,89 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   }
   const bool has_nan = FLAGS && uniform(nan != 0);
   pin(x);
+  // Batcher's odd-even merge of A (wave 0) and B (wave 1), split by parity:
+  // v = merge(A_even, B_even) in wave 0, w = merge(A_odd, B_odd) in wave 1,
+  // and the merged order is c_0 = v_0, c_{2i-1} = min(v_i, w_{i-1}),
+  // c_{2i} = max(v_i, w_{i-1}).  Each wave hands the parity it does not merge
+  // to the other (64 keys, 16 KB): wave 0 A_odd through R0, wave 1 B_even
+  // through R1.
+  Img r0 = im, r1 = im + kHalf / 8 * 64;
   {
-    // each wave hands over its upper 64 (groups 16..31) into its own half of
-    // the image: region R0 = A's (wave 0), R1 = B's (wave 1)
-    Img mine = im + (h == 0 ? 0 : kHalf / 8 * 64);
+    Img mine = h == 0 ? r0 : r1;
+    const int par = h == 0 ? 1 : 0;
 #pragma unroll
-    for (int g = kHalf / 8; g < kHalf / 4; ++g)
-      mine[(g - kHalf / 8) * 64 + lane] =
-          u32x4{raw(x[4 * g]), raw(x[4 * g + 1]), raw(x[4 * g + 2]), raw(x[4 * g + 3])};
+    for (int g = 0; g < kHalf / 8; ++g)
+      mine[g * 64 + lane] = u32x4{raw(x[8 * g + par]), raw(x[8 * g + 2 + par]), raw(x[8 * g + 4 + par]),
+                                  raw(x[8 * g + 6 + par])};
   }
   if constexpr (FLAGS) {
     if (lane == 0) flags[h] = has_nan ? 1 : 0;
   }
-  block_sync();  // 1: A in the image
+  block_sync();  // 1: both parities in the image
   if constexpr (FLAGS) {
     if (uniform((flags[0] | flags[1]) != 0)) return pair_keys<RULE>(P, c0, lane_off, im, h, lane);
   }
   {
-    constexpr int b = (2 * kHalf * 2) / 10;  // 51
-    constexpr int hi = 2 * kHalf - b;        // 205: ranks b..hi-1 kept
+    constexpr int b = (2 * kHalf * 2) / 10;  // 51: ranks b..2*kHalf-b-1 = 51..204 kept
     constexpr int Q = kHalf / 2;             // 64
+    constexpr int I0 = (b + 1) / 2;          // 26: c_51 = min(v_26, w_25)
+    constexpr int IM = kHalf / 2;            // 64: c_127 = min(v_64, w_63), c_128 = max(...)
+    constexpr int I1 = kHalf - I0;           // 102: c_204 = max(v_102, w_101)
+    constexpr int NX = IM - I0 + 1;          // 39 values cross per wave
     auto part = (float __attribute__((address_space(3)))*)(im + kHalf / 4 * 64);
-    // The flip split like the median: wave 1 takes the pairs (B_j, A_{127-j})
-    // for j < 64 (A's upper half from R0), wave 0 the pairs (A_i, B_{127-i})
-    // for i < 64 (B's upper half from R1), i.e. j = 127 - i >= 64.  Wave 1
-    // keeps L and sends its U_0..63 through R0; wave 0 keeps U and sends its
-    // L_64..127 through R1 (each wave rewrites only the region it read).
-    Img other = im + (h == 0 ? kHalf / 8 * 64 : 0);
-    if (h == 1) flip_half<true>(other, x, lane);  // wave 1: L_j at x[j], U_j parked at x[64 + j]
-    else flip_half<false>(other, x, lane);        // wave 0: U_{127-i} at x[i], L_{127-i} parked at x[64 + i]
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the region is read before it is rewritten
+    // wave 0 sends v_26..v_64 through R1, wave 1 w_63..w_101 through R0 --
+    // each rewrites only the region it read (constant indices: a runtime
+    // offset into m would put m in scratch)
+    T m[kHalf];
+    if (h == 0) {  // v = merge(A_even, B_even): ranks I0..I1 of it
 #pragma unroll
-    for (int g = 0; g < Q / 4; ++g)  // wave 1: U_j (j < 64) in slot g; wave 0: L_{127-i} (i < 64) in slot g
-      other[g * 64 + lane] = u32x4{raw(x[Q + 4 * g]), raw(x[Q + 4 * g + 1]), raw(x[Q + 4 * g + 2]), raw(x[Q + 4 * g + 3])};
-    block_sync();  // 2: both parts handed over
-    if (h == 1) {  // L_64..127 = wave 0's L_{127-i}, i = 127 - j, from R1
-      Img r1 = im + kHalf / 8 * 64;
+      for (int j = 0; j < Q; ++j) {
+        m[j] = x[2 * j];
+        m[Q + j] = from_raw<T>(img_at(r1, j, lane));
+      }
+      net_merge128_r26_102<true>(m);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      send_run<I0, NX>(r1, m, lane);
+    } else {       // w = merge(A_odd, B_odd): ranks I0-1..I1-1
 #pragma unroll
-      for (int j = Q; j < kHalf; ++j) x[j] = from_raw<T>(img_at(r1, kHalf - 1 - j, lane));
-      net_bmerge128_r51_127<true>(x);
-      part[lane] = sum_ranks<b, kHalf>(x, 0.f);
+      for (int j = 0; j < Q; ++j) {
+        m[j] = from_raw<T>(img_at(r0, j, lane));
+        m[Q + j] = x[2 * j + 1];
+      }
+      net_merge128_r25_101<true>(m);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      send_run<IM - 1, NX>(r0, m, lane);
+    }
+    block_sync();  // 2: the crossing values in the image
+    if (h == 1) {  // c_51..c_127, ascending sum from +0
+      T c[2 * (IM - I0) + 1];
+#pragma unroll
+      for (int i = I0; i < IM; ++i) {
+        const T vi = from_raw<T>(img_at(r1, i - I0, lane));
+        c[2 * (i - I0)] = min(vi, m[i - 1]);
+        c[2 * (i - I0) + 1] = max(vi, m[i - 1]);
+      }
+      c[2 * (IM - I0)] = min(from_raw<T>(img_at(r1, IM - I0, lane)), m[IM - 1]);
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 2 * (IM - I0) + 1; ++k) acc = __fadd_rn(acc, val(c[k]));
+      part[lane] = acc;
       block_sync();  // 3: the partial sum of ranks 51..127 in its slot
       return 0.f;
     }
-    T u[kHalf];  // U_j: j < 64 from wave 1 through R0, j >= 64 kept at x[127 - j]
+    T c[2 * (I1 - IM) + 1];  // c_128..c_204
+    c[0] = max(m[IM], from_raw<T>(img_at(r0, 0, lane)));
 #pragma unroll
-    for (int j = 0; j < Q; ++j) u[j] = from_raw<T>(img_at(im, j, lane));
-#pragma unroll
-    for (int j = Q; j < kHalf; ++j) u[j] = x[kHalf - 1 - j];
-    net_bmerge128_r0_76<true>(u);
+    for (int i = IM + 1; i <= I1; ++i) {
+      const T wi = from_raw<T>(img_at(r0, i - IM, lane));  // w_{i-1}
+      c[2 * (i - IM) - 1] = min(m[i], wi);
+      c[2 * (i - IM)] = max(m[i], wi);
+    }
     block_sync();  // 3
-    return sum_ranks<0, hi - kHalf>(u, part[lane]) / static_cast<float>(hi - b);
+    float acc = part[lane];
+#pragma unroll
+    for (int k = 0; k < 2 * (I1 - IM) + 1; ++k) acc = __fadd_rn(acc, val(c[k]));
+    return acc / static_cast<float>(2 * kHalf - 2 * b);
   }
 }
 
@@ -338,7 +323,7 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
   uint32_t v[kHalf];
   load_half(v, P, c0, lane_off, h);
   if constexpr (RULE == P2P_RULE_MEDIAN) return median_pair<uint32_t>(v, im, h, lane);
-  else return pair_body<RULE, uint32_t>(v, im, h, lane);
+  else return pair_body<RULE, kx>(v, im, h, lane);  // kx: max as a ^ b ^ min, fewer live values
 }
 
 // One 64-coordinate tile of the pair kernels.  SMALL (flat buffers below
@@ -380,7 +365,8 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
   }
 }
 
-// Trimmed mean: 32 KB image + the partial sums (256 B), 2 waves per SIMD.
+// Trimmed mean: two 16 KB parity regions + the partial sums (256 B), 2 waves
+// per SIMD.
 template <bool SEGS, bool SMALL = false>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(
     const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n, float* w,

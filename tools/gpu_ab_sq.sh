@@ -52,6 +52,6 @@ for f in sorted(glob.glob(os.path.join(sys.argv[1], "sq_*.json"))):
     d = json.load(open(f))
     for p in d.get("pmc", []):
         print(os.path.basename(f), "valu/wave=%.1f" % p.get("valu_insts_per_wave", 0), "clock=%.3f GHz" % p.get("effective_clock_ghz", 0),
-              "kernel_us=%.1f" % ([k["avg_ns"] for k in d["kernels"] if k["name"] == p["kernel"]] or [0])[0] / 1e3)
+              "kernel_us=%.1f" % (([k["avg_ns"] for k in d["kernels"] if k["name"] == p["kernel"]] or [0])[0] / 1e3))
 PY
 ls "$OUT"
