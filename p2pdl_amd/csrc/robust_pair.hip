@@ -214,14 +214,19 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   // c_{2i} = max(v_i, w_{i-1}).  Each wave hands the parity it does not merge
   // to the other (64 keys, 16 KB): wave 0 A_odd through R0, wave 1 B_even
   // through R1.
+  // (constant register indices on each side; the asm keeps LLVM from merging
+  // the two sides' stores into one store of v_cndmask selects, one per key)
   Img r0 = im, r1 = im + kHalf / 8 * 64;
-  {
-    Img mine = h == 0 ? r0 : r1;
-    const int par = h == 0 ? 1 : 0;
+  if (h == 0) {
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int g = 0; g < kHalf / 8; ++g)
-      mine[g * 64 + lane] = u32x4{raw(x[8 * g + par]), raw(x[8 * g + 2 + par]), raw(x[8 * g + 4 + par]),
-                                  raw(x[8 * g + 6 + par])};
+      r0[g * 64 + lane] = u32x4{raw(x[8 * g + 1]), raw(x[8 * g + 3]), raw(x[8 * g + 5]), raw(x[8 * g + 7])};
+  } else {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int g = 0; g < kHalf / 8; ++g)
+      r1[g * 64 + lane] = u32x4{raw(x[8 * g]), raw(x[8 * g + 2]), raw(x[8 * g + 4]), raw(x[8 * g + 6])};
   }
   if constexpr (FLAGS) {
     if (lane == 0) flags[h] = has_nan ? 1 : 0;
