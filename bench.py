@@ -276,7 +276,7 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
             what = "torch.sort(dim=0) + ascending sum of the kept ranks (the build-defined rule on CPU)"
         cpu = cpu_record(res, "GB/s", "port", f"{K} peers x {n_s:,} fp32 coords, {what}, "
                                               f"{res['reps']} reps in {res['seconds']}s")
-    dtype = "fp32" if rule == "fedavg" else "fp32 (u32 total-order keys)"
+    dtype = "fp32" if rule == "fedavg" else "fp32 (IEEE total order: f32 min/max/med3 networks, u32 keys for NaN tiles)"
     rec = {
         "workload": name, "value": round(K * n * 4 * world / step_s / 1e9, 2), "unit": "GB/s",
         "ms_per_step": round(step_s * 1e3, 4), "steps": steps, "scaling": "weak", "dtype": dtype,
