@@ -466,6 +466,63 @@ def test_trimmed_explicit_b(cuda, k, b):
     assert_bits_equal(host(out), out_ref, what=f"trim K={k} b={b}")
 
 
+def structured_peers(k, seed):
+    """Coordinate blocks of 64 (one pair-kernel tile / one wave each) that
+    drive the merges to their extremes: the first half of the peers all below
+    the second half and the reverse (one side of every parity / two-set merge
+    empty), interleaved ranks, all equal, ties exactly at the trim boundaries,
+    +-0 only, +-inf and the largest finites at the kept-rank edges, peers in
+    descending order, denormals only."""
+    rng = np.random.default_rng(seed)
+    b = int(0.2 * k + 1e-9)
+    base = np.arange(k, dtype=np.float32)
+    cols = []
+    def add(col):
+        cols.append(np.asarray(col, dtype=np.float32))
+    for _ in range(64):
+        add(base * 1e-3)                                  # A < B (peers 0..k/2-1 smallest)
+    for _ in range(64):
+        add(base[::-1] * 1e-3)                            # A > B
+    for _ in range(64):
+        add(np.where(np.arange(k) % 2 == 0, base, -base) * 1e-2)  # interleaved signs
+    for _ in range(64):
+        add(np.full(k, 0.375))                            # all equal
+    for _ in range(64):                                   # ties straddling ranks b-1 / b and k-b-1 / k-b
+        v = rng.standard_normal(k).astype(np.float32)
+        v = np.sort(v)
+        v[b - 2:b + 2] = v[b]
+        v[k - b - 2:k - b + 2] = v[k - b - 1]
+        add(rng.permutation(v))
+    for _ in range(64):
+        add(rng.choice(np.array([0.0, -0.0], dtype=np.float32), size=k))  # signed zeros only
+    for _ in range(64):                                   # infinities / extremes at the kept edges
+        v = rng.standard_normal(k).astype(np.float32)
+        v[: b + 1] = -np.inf
+        v[k - b - 1:] = np.float32(np.finfo(np.float32).max)
+        add(rng.permutation(v))
+    for _ in range(64):
+        add((rng.integers(1, 50, size=k) * np.float32(1e-45)).astype(np.float32))  # denormals
+    x = np.stack(cols, axis=1)  # (k, 512)
+    return [np.ascontiguousarray(x[p]) for p in range(k)]
+
+
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+@pytest.mark.parametrize("k", [64, 128, 256])
+def test_robust_structured_extremes(cuda, rule, k):
+    """The pair kernel's parity merge / two-set search and the one-lane
+    networks on inputs that push every merge to an extreme (bit-exact)."""
+    peers = structured_peers(k, 7 * k)
+    n = peers[0].size
+    w = oracle.synth(n, 5, 0xFFFFF, 5e-2)
+    r = ops.rule_id(rule)
+    b = ops.trim_count(k) if rule == "trimmed" else 0
+    w_ref, out_ref = oracle.robust(peers, r, b, w=w)
+    wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate([to_dev(p, cuda) for p in peers], rule, w=wt, out=out, trim_b=b)
+    assert_bits_equal(host(out), out_ref, nan_equal=(rule != "median"), what=f"{rule} K={k} structured")
+    assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k} structured")
+
+
 def test_robust_matches_torch_median(cuda):
     """Independent pin for NaN-free data: torch.median's lower median."""
     k, n = 64, 20000
