@@ -110,6 +110,16 @@ def check(rc: int, what: str) -> None:
 
 
 def stream_handle(device=None) -> int:
+    """The raw hipStream_t of the current stream of ``device`` (default: the
+    current device) -- what torch.cuda.current_stream(device).cuda_stream
+    returns, without building the Stream object (a few us per launch at the
+    reference's MLP size, where the whole call is host-bound)."""
     import torch
 
-    return torch.cuda.current_stream(device).cuda_stream
+    if device is None:
+        idx = torch.cuda.current_device()
+    elif isinstance(device, int):
+        idx = device
+    else:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)

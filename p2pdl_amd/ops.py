@@ -207,8 +207,9 @@ class _NoCtx:
 _NO_CTX = _NoCtx()
 
 
-def _launch_table(base: int, L: int, tiles: int, K: int, r: int, b: int, lr: float) -> None:
-    N.check(N.lib().p2p_aggregate_segments_f32(base, L, tiles, K, r, b, lr, N.stream_handle()),
+def _launch_table(base: int, L: int, tiles: int, K: int, r: int, b: int, lr: float, stream=None) -> None:
+    N.check(N.lib().p2p_aggregate_segments_f32(base, L, tiles, K, r, b, lr,
+                                               N.stream_handle() if stream is None else stream),
             "p2p_aggregate_segments_f32")
 
 
@@ -322,10 +323,10 @@ def aggregate_ptr_table_(ws: Sequence[torch.Tensor], ptrs: np.ndarray, rule="fed
     if hit is not None:
         buf, tiles, r, b, alloc_stream = hit
         with torch.cuda.device(dev) if torch.cuda.current_device() != dev.index else _NO_CTX:
-            stream = torch.cuda.current_stream(dev)
-            if stream.cuda_stream != alloc_stream:
-                buf.record_stream(stream)
-            _launch_table(buf.data_ptr(), L, tiles, K, r, b, lr)
+            raw = N.stream_handle(dev)
+            if raw != alloc_stream:
+                buf.record_stream(torch.cuda.current_stream(dev))
+            _launch_table(buf.data_ptr(), L, tiles, K, r, b, lr, stream=raw)
         return
     _launch_segments(ws, ptrs, numels, rule, K, lr, trim_b, trim_frac, None, dev, cache_key=key)
 
@@ -360,10 +361,10 @@ def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: S
     if hit is not None:  # same addresses and sizes as a previous call: same table
         buf, tiles, r, b, alloc_stream = hit
         with torch.cuda.device(dev) if torch.cuda.current_device() != dev.index else _NO_CTX:
-            stream = torch.cuda.current_stream(dev)
-            if stream.cuda_stream != alloc_stream:
-                buf.record_stream(stream)  # eviction must not recycle it under this launch
-            _launch_table(buf.data_ptr(), L, tiles, K, r, b, lr)
+            raw = N.stream_handle(dev)
+            if raw != alloc_stream:
+                buf.record_stream(torch.cuda.current_stream(dev))  # eviction must not recycle it under this launch
+            _launch_table(buf.data_ptr(), L, tiles, K, r, b, lr, stream=raw)
         return
     rows_a = np.asarray(rows, dtype=np.int64)
     offs_a = np.asarray(offsets, dtype=np.int64)
