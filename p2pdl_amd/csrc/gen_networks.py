@@ -115,6 +115,8 @@ def batcher_stages(n: int, lo: int = 0):
     irregular layers leave fewer minima / maxima for a consumer to absorb."""
     if n == 1:
         return []
+    if n == 4:  # the three-input 4-sorter (7 instructions; Batcher's 5 comparators lower to 9)
+        return [((lo, lo + 1, lo + 2, lo + 3), ("all", lo, 4))]
     h = n // 2
     return (batcher_stages(h, lo) + batcher_stages(h, lo + h)
             + [(c, ("merge", lo, n)) for c in oddeven_merge(lo, lo + n - 1, 1)])
@@ -180,10 +182,18 @@ def domain_bits(kind, n):
 
 def prune(tagged, wanted):
     """Backward liveness.  Returns ((op, a, b), stage) with op in {CE, MIN, MAX}.
-    MIN: v[a] = min(v[a], v[b]);  MAX: v[b] = max(v[a], v[b])."""
+    MIN: v[a] = min(v[a], v[b]);  MAX: v[b] = max(v[a], v[b]).  A 4-sorter
+    ((a, b, c, d), stage) stays whole while any of its outputs is live (its
+    dead outputs are dropped later, by the SSA liveness of Program)."""
     live = set(wanted)
     out = []
-    for (a, b), st in reversed(tagged):
+    for wires, st in reversed(tagged):
+        if len(wires) == 4:
+            if live.intersection(wires):
+                out.append((("SORT4",) + tuple(wires), st))
+                live.update(wires)
+            continue
+        a, b = wires
         la, lb = a in live, b in live
         if la and lb:
             out.append((("CE", a, b), st))
@@ -202,7 +212,13 @@ def prune(tagged, wanted):
 def apply(ops, vals):
     """Runs a pruned comparator list (classic form) on vals."""
     v = list(vals)
-    for (op, a, b), _ in ops:
+    for op_, _ in ops:
+        if op_[0] == "SORT4":
+            w = op_[1:]
+            for i, x in zip(w, sorted(v[j] for j in w)):
+                v[i] = x
+            continue
+        op, a, b = op_
         lo, hi = min(v[a], v[b]), max(v[a], v[b])
         if op == "CE":
             v[a], v[b] = lo, hi
@@ -223,7 +239,18 @@ class Program:
         self.args = [()] * kp
         self.stage = [None] * kp
         wire = list(range(kp))
-        for (op, a, b), st in ops:
+        for op_, st in ops:
+            if op_[0] == "SORT4":  # sort3(a, b, c), then d inserted by med3
+                a, b, c, d = (wire[w] for w in op_[1:])
+                t0 = self._node("lo3", (a, b, c), st)
+                t1 = self._node("med3", (a, b, c), st)
+                t2 = self._node("hi3", (a, b, c), st)
+                ys = (self._node("lo", (t0, d), st), self._node("med3", (t0, t1, d), st),
+                      self._node("med3", (t1, t2, d), st), self._node("hi", (t2, d), st))
+                for w, y in zip(op_[1:], ys):
+                    wire[w] = y
+                continue
+            op, a, b = op_
             va, vb = wire[a], wire[b]
             if op in ("CE", "MIN"):
                 wire[a] = self._node("lo", (va, vb), st)
@@ -241,8 +268,14 @@ class Program:
         stage_in = {}
         wire = list(range(kp))
         node = kp
-        for (op, a, b), st in ops:
+        for op_, st in ops:
             stage_in.setdefault(st, list(wire))
+            if op_[0] == "SORT4":
+                for k, w in enumerate(op_[1:]):
+                    wire[w] = node + 3 + k
+                node += 7
+                continue
+            op, a, b = op_
             if op in ("CE", "MIN"):
                 wire[a] = node
                 node += 1
@@ -254,8 +287,14 @@ class Program:
             b = {w[lo + j]: m for j, m in enumerate(domain_bits(st[0], n))}
             for i in range(kp, len(self.kind)):
                 if self.stage[i] == st:
-                    x, y = self.args[i]
-                    b[i] = b[x] & b[y] if self.kind[i] == "lo" else b[x] | b[y]
+                    xs = [b[a] for a in self.args[i]]
+                    k = self.kind[i]
+                    if k in ("lo", "lo3"):
+                        b[i] = xs[0] & xs[1] & (xs[2] if len(xs) > 2 else -1)
+                    elif k in ("hi", "hi3"):
+                        b[i] = xs[0] | xs[1] | (xs[2] if len(xs) > 2 else 0)
+                    else:  # med3 = majority
+                        b[i] = (xs[0] & xs[1]) | (xs[0] & xs[2]) | (xs[1] & xs[2])
             self.bits[st] = b
         self.absorbed = {}  # consumer -> the operand node it absorbs
         self.elim = set()
@@ -293,6 +332,8 @@ class Program:
         for e in (reversed(order) if reverse else order):
             if e in outs or e in must or e in self.absorbed or not cons[e]:
                 continue
+            if self.kind[e] not in ("lo", "hi") or any(self.kind[c] not in ("lo", "hi") for c in cons[e]):
+                continue  # a three-input node can neither be absorbed nor absorb
             if any(c in self.absorbed or c in self.elim for c in cons[e]):
                 continue
             if any(a in self.elim for a in self.args[e]):
@@ -318,6 +359,9 @@ class Program:
         lo_of = {}
         for i in sorted(self.live):
             if self.kind[i] == "in" or i in self.elim:
+                continue
+            if self.kind[i] in ("lo3", "hi3", "med3"):
+                out.append((i, self.kind[i], self.args[i]))
                 continue
             if i in self.absorbed:
                 e = self.absorbed[i]
@@ -429,10 +473,10 @@ def emit_fused():
     for tag, kp, wanted, base in network_specs():
         ops, prog = build(tag, kp, wanted, base)
         ins = prog.instrs()
-        nce = sum(1 for (o, _, _), _ in ops if o == "CE")
+        nce = sum(1 for o, _ in ops if o[0] == "CE") + 5 * sum(1 for o, _ in ops if o[0] == "SORT4")
         cnt = {k: sum(1 for _, op, _ in ins if op == k) for k in ("lo3", "hi3", "med3")}
         lines.append(f"// {tag}: KP={kp} wanted={'all' if wanted is None else f'{wanted[0]}..{wanted[-1]}'}"
-                     f" comparators={nce} two-input valu={2 * nce + len(ops) - nce} -> {len(ins)}"
+                     f" comparators={nce} two-input valu={2 * nce + sum(1 for o, _ in ops if o[0] in ('MIN', 'MAX'))} -> {len(ins)}"
                      f" (min3 {cnt['lo3']}, max3 {cnt['hi3']}, med3 {cnt['med3']})")
         lines.append("template <bool ASC, typename T, typename H = NoHook>  // ASC=false sorts descending")
         lines.append(f"__device__ __forceinline__ void net_{tag}(T (&v)[{kp}], H&& hook = H{{}}) {{")
