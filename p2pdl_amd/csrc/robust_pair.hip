@@ -80,16 +80,19 @@ __device__ __forceinline__ void store_half(Img im, const T (&x)[kHalf], int lane
     im[g * 64 + lane] = u32x4{raw(x[4 * g]), raw(x[4 * g + 1]), raw(x[4 * g + 2]), raw(x[4 * g + 3])};
 }
 
-// m[FIRST .. FIRST+N-1] as elements 0..N-1 of an image region.
+// Word image of the trimmed path: element j of lane l at word j*64 + l.  A
+// pair of rows is one ds_write2st64_b32 / ds_read2st64_b32 from / into ANY
+// two VGPRs, conflict-free -- the b128 image needs its 4 words in consecutive
+// VGPRs, and a network's outputs are not: 64 v_mov per wave on the hand-off.
+using W32 = uint32_t __attribute__((address_space(3)))*;
+
+__device__ __forceinline__ uint32_t row_at(W32 im, int j, int lane) { return im[j * 64 + lane]; }
+
+// m[FIRST .. FIRST+N-1] as rows 0..N-1 of a word image.
 template <int FIRST, int N, typename T>
-__device__ __forceinline__ void send_run(Img dst, const T (&m)[kHalf], int lane) {
+__device__ __forceinline__ void send_run(W32 dst, const T (&m)[kHalf], int lane) {
 #pragma unroll
-  for (int g = 0; g < (N + 3) / 4; ++g) {
-    u32x4 q;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = 4 * g + k < N ? raw(m[FIRST + 4 * g + k]) : 0u;
-    dst[g * 64 + lane] = q;
-  }
+  for (int j = 0; j < N; ++j) dst[j * 64 + lane] = raw(m[FIRST + j]);
 }
 
 __device__ __forceinline__ void block_sync() {
@@ -214,19 +217,17 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   // c_{2i} = max(v_i, w_{i-1}).  Each wave hands the parity it does not merge
   // to the other (64 keys, 16 KB): wave 0 A_odd through R0, wave 1 B_even
   // through R1.
-  // (constant register indices on each side; the asm keeps LLVM from merging
-  // the two sides' stores into one store of v_cndmask selects, one per key)
-  Img r0 = im, r1 = im + kHalf / 8 * 64;
+  // (the distinct asm after each side's stores keeps LLVM from sinking both
+  // into one store sequence fed by moves or selects)
+  W32 r0 = reinterpret_cast<W32>(im), r1 = r0 + kHalf / 2 * 64;
   if (h == 0) {
-    asm volatile("" ::: "memory");
 #pragma unroll
-    for (int g = 0; g < kHalf / 8; ++g)
-      r0[g * 64 + lane] = u32x4{raw(x[8 * g + 1]), raw(x[8 * g + 3]), raw(x[8 * g + 5]), raw(x[8 * g + 7])};
+    for (int j = 0; j < kHalf / 2; ++j) r0[j * 64 + lane] = raw(x[2 * j + 1]);
+    asm volatile("; parity hand-off, wave 0" ::: "memory");
   } else {
-    asm volatile("" ::: "memory");
 #pragma unroll
-    for (int g = 0; g < kHalf / 8; ++g)
-      r1[g * 64 + lane] = u32x4{raw(x[8 * g]), raw(x[8 * g + 2]), raw(x[8 * g + 4]), raw(x[8 * g + 6])};
+    for (int j = 0; j < kHalf / 2; ++j) r1[j * 64 + lane] = raw(x[2 * j]);
+    asm volatile("; parity hand-off, wave 1" ::: "memory");
   }
   if constexpr (FLAGS) {
     if (lane == 0) flags[h] = has_nan ? 1 : 0;
@@ -251,7 +252,7 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
 #pragma unroll
       for (int j = 0; j < Q; ++j) {
         m[j] = x[2 * j];
-        m[Q + j] = from_raw<T>(img_at(r1, j, lane));
+        m[Q + j] = from_raw<T>(row_at(r1, j, lane));
       }
       net_merge128_r26_102<true>(m);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -259,7 +260,7 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
     } else {       // w = merge(A_odd, B_odd): ranks I0-1..I1-1
 #pragma unroll
       for (int j = 0; j < Q; ++j) {
-        m[j] = from_raw<T>(img_at(r0, j, lane));
+        m[j] = from_raw<T>(row_at(r0, j, lane));
         m[Q + j] = x[2 * j + 1];
       }
       net_merge128_r25_101<true>(m);
@@ -271,11 +272,11 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
       T c[2 * (IM - I0) + 1];
 #pragma unroll
       for (int i = I0; i < IM; ++i) {
-        const T vi = from_raw<T>(img_at(r1, i - I0, lane));
+        const T vi = from_raw<T>(row_at(r1, i - I0, lane));
         c[2 * (i - I0)] = min(vi, m[i - 1]);
         c[2 * (i - I0) + 1] = max(vi, m[i - 1]);
       }
-      c[2 * (IM - I0)] = min(from_raw<T>(img_at(r1, IM - I0, lane)), m[IM - 1]);
+      c[2 * (IM - I0)] = min(from_raw<T>(row_at(r1, IM - I0, lane)), m[IM - 1]);
       float acc = 0.f;
 #pragma unroll
       for (int k = 0; k < 2 * (IM - I0) + 1; ++k) acc = __fadd_rn(acc, val(c[k]));
@@ -284,10 +285,10 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
       return 0.f;
     }
     T c[2 * (I1 - IM) + 1];  // c_128..c_204
-    c[0] = max(m[IM], from_raw<T>(img_at(r0, 0, lane)));
+    c[0] = max(m[IM], from_raw<T>(row_at(r0, 0, lane)));
 #pragma unroll
     for (int i = IM + 1; i <= I1; ++i) {
-      const T wi = from_raw<T>(img_at(r0, i - IM, lane));  // w_{i-1}
+      const T wi = from_raw<T>(row_at(r0, i - IM, lane));  // w_{i-1}
       c[2 * (i - IM) - 1] = min(m[i], wi);
       c[2 * (i - IM)] = max(m[i], wi);
     }
