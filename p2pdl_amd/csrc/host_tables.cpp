@@ -53,6 +53,11 @@ PyObject* gather_peer_table(PyObject*, PyObject* args) {
                         &numels_obj, &device, &out))
     return nullptr;
   const Py_ssize_t K = PyList_GET_SIZE(received), L = PyList_GET_SIZE(keys);
+  if (out.len < static_cast<Py_ssize_t>(sizeof(uint64_t)) * L * K || PyList_GET_SIZE(numels_obj) != L) {
+    PyBuffer_Release(&out);
+    PyErr_SetString(PyExc_ValueError, "gather_peer_table: buffer / numels do not match L x K");
+    return nullptr;
+  }
   int status = 0;
   std::vector<int64_t> numels(static_cast<size_t>(L));
   for (Py_ssize_t l = 0; l < L; ++l) {
@@ -61,11 +66,6 @@ PyObject* gather_peer_table(PyObject*, PyObject* args) {
       PyBuffer_Release(&out);
       return nullptr;
     }
-  }
-  if (out.len < static_cast<Py_ssize_t>(sizeof(uint64_t)) * L * K || PyList_GET_SIZE(numels_obj) != L) {
-    PyBuffer_Release(&out);
-    PyErr_SetString(PyExc_ValueError, "gather_peer_table: buffer / numels do not match L x K");
-    return nullptr;
   }
   uint64_t* table = static_cast<uint64_t*>(out.buf);
   for (Py_ssize_t j = 0; j < K && status == 0; ++j) {

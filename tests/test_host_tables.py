@@ -1,0 +1,41 @@
+"""CPU checks of the drop-in's C gather of the peer table
+(p2pdl_amd/csrc/host_tables.cpp): the lookups raise what the reference's
+``received_models[j]["model"][key]`` raises (aggregator/aggregation.py:25-28),
+anything the C path cannot vouch for returns 1 (the Python path diagnoses it),
+and mismatched sizes are rejected before any list element is read."""
+import numpy as np
+import pytest
+import torch
+
+_host_tables = pytest.importorskip("p2pdl_amd._host_tables")
+
+
+def _table(L, K):
+    return np.zeros((L, K), dtype=np.uint64)
+
+
+def test_missing_key_raises_keyerror():
+    received = [{"model": {"a": torch.zeros(2)}}]
+    with pytest.raises(KeyError):
+        _host_tables.gather_peer_table(received, ["b", "a"], [2, 2], 0, _table(2, 1))
+
+
+def test_record_without_model_raises_keyerror():
+    with pytest.raises(KeyError):
+        _host_tables.gather_peer_table([{"sender": 1}], ["a"], [2], 0, _table(1, 1))
+
+
+def test_host_tensors_defer_to_python_path():
+    received = [{"model": {"a": torch.zeros(2)}}, {"model": {"a": torch.zeros(2)}}]
+    assert _host_tables.gather_peer_table(received, ["a"], [2], 0, _table(1, 2)) == 1
+
+
+def test_non_tensor_defers_to_python_path():
+    assert _host_tables.gather_peer_table([{"model": {"a": [0.0, 1.0]}}], ["a"], [2], 0, _table(1, 1)) == 1
+
+
+@pytest.mark.parametrize("numels, shape", [([2], (2, 1)), ([2, 2], (1, 1))])
+def test_size_mismatch_rejected(numels, shape):
+    received = [{"model": {"a": torch.zeros(2), "b": torch.zeros(2)}}]
+    with pytest.raises(ValueError):
+        _host_tables.gather_peer_table(received, ["a", "b"], numels, 0, np.zeros(shape, dtype=np.uint64))
