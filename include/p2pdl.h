@@ -32,8 +32,9 @@ extern "C" {
 #endif
 
 /* 2: p2p_set_robust_layout (a process-global A/B switch of version 1) is
- *    gone; every other entry point is unchanged. */
-#define P2P_ABI_VERSION 2
+ *    gone; every other entry point is unchanged.
+ * 3: adds p2p_land_segments_f32 (K5, landing a received update). */
+#define P2P_ABI_VERSION 3
 
 typedef void *p2p_stream_t; /* hipStream_t */
 
@@ -133,6 +134,25 @@ typedef struct p2p_delta_segment_t {
 /* Whole state_dict in one launch (segs is a DEVICE array). */
 int32_t p2p_delta_snapshot_segments_f32(const p2p_delta_segment_t *segs, int32_t nseg, int64_t total_tiles,
                                         int32_t first, p2p_stream_t stream);
+
+/* ---- K5: landing a received update ---------------
+ * Replaces the per-tensor unpickling of reference node/node.py:135-141 for the
+ * fp32 payloads of one serialized update: msg is the whole message, copied
+ * to the device as bytes (msg_bytes of them); segment j copies n fp32 values
+ * from byte offset src_off of msg (any alignment) to dst (4-B aligned, e.g.
+ * a tensor's offset in its slab row).  Reads stay below msg_bytes. */
+#define P2P_LAND_TILE 4096 /* fp32 values per tile of the landing kernel */
+
+typedef struct p2p_land_segment_t {
+  uint64_t src_off;   /* byte offset of the payload in msg */
+  float *dst;         /* destination of n fp32 values */
+  int64_t n;
+  int64_t tile_begin; /* sum of ceil(n_j / P2P_LAND_TILE) over earlier segments */
+} p2p_land_segment_t;
+
+/* One launch per update (segs is a DEVICE array of nseg entries). */
+int32_t p2p_land_segments_f32(const uint8_t *msg, uint64_t msg_bytes, const p2p_land_segment_t *segs,
+                              int32_t nseg, int64_t total_tiles, p2p_stream_t stream);
 
 /* ---- K3: SHA-256 over serialized updates --------------------------------
  * digests[32*i .. 32*i+31] = SHA-256(msgs[i][0 .. lens[i]-1]) (FIPS 180-4),

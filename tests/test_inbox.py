@@ -566,3 +566,118 @@ def test_slab_table_cache_across_rounds_and_streams(cuda, monkeypatch):
         w = want
     mine = [key for key in ops._TABLES if key[1:3] == (inbox.slab.data_ptr(), k + 1)]
     assert len(mine) == 2  # one table per row set (0..3, 1..4), reused across rounds and streams
+
+
+# ---- K5 device path: the message in pinned memory, one DMA, the landing kernel
+def _pinned(inbox, data):
+    m = inbox.message_buffer(len(data))
+    m.buf[:len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    return m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto", [3, 4, 5])
+def test_pinned_landing_matches_pickle_loads(cuda, proto):
+    """p2p_land_segments_f32 places every payload (arbitrary byte offsets in
+    the pickle: the 0-d / int64 BatchNorm entries shift them) bit-exactly;
+    non-fp32 entries become their own tensors as on the staging path."""
+    net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.BatchNorm1d(5), torch.nn.Linear(5, 3))
+    rows = []
+    for j in range(4):
+        torch.manual_seed(j)
+        sd = {k: (v + torch.randn_like(v) if v.is_floating_point() else v + j) for k, v in net.state_dict().items()}
+        sd.update({f"x{j}.w": torch.randn(1 + j, 37)})  # extra key: not in the template, small tensor
+        rows.append(pickle.dumps(sd, protocol=proto))
+    template = {k: v.to(cuda) for k, v in net.state_dict().items()}
+    inbox = DeviceInbox(template, k_max=4, device=cuda)
+    got = [inbox.land(_pinned(inbox, d)) for d in rows]
+    torch.cuda.synchronize()
+    for d, g in zip(rows, got):
+        ref = pickle.loads(d)
+        assert list(g) == list(ref)
+        for key in ref:
+            assert g[key].is_cuda and g[key].dtype == ref[key].dtype and g[key].shape == ref[key].shape, key
+            assert torch.equal(g[key].cpu(), ref[key]), key
+    assert all(set(g.slab_keys) == {k for k, v in template.items() if v.dtype == torch.float32} for g in got)
+
+
+@pytest.mark.gpu
+def test_pinned_landing_every_misalignment_and_tail(cuda):
+    """Payload offsets mod 4 = 0..3 (a prefix key of 1..4 bytes of name moves
+    them) and a tensor ending at the last payload byte of the message."""
+    for pad in range(1, 5):
+        upd = collections.OrderedDict([("p" * pad, torch.arange(3, dtype=torch.float32)),
+                                       ("w", torch.randn(4099)), ("b", torch.randn(1))])
+        data = pickle.dumps(upd)
+        template = {k: torch.zeros_like(v, device=cuda) for k, v in upd.items()}
+        inbox = DeviceInbox(template, k_max=1, device=cuda)
+        got = inbox.land(_pinned(inbox, data), 0)
+        torch.cuda.synchronize()
+        for key, v in upd.items():
+            assert_bits_equal(got[key].cpu().numpy(), v.numpy(), what=f"pad {pad} {key}")
+
+
+@pytest.mark.gpu
+def test_pinned_landing_resnet_sized_update_and_digest(cuda):
+    """Large conv / fc payloads (2.9M params, multi-tile segments): the
+    landing kernel vs pickle.loads, the overlapped digest vs hashlib, pinned
+    buffers reused from the pool across rounds."""
+    import hashlib
+
+    shapes = [("conv.weight", (64, 3, 7, 7)), ("fc.weight", (1000, 512)), ("fc.bias", (1000,))] + \
+        [(f"layer{i}.weight", (128, 128, 3, 3)) for i in range(4)]
+    template = {k: torch.zeros(s, device=cuda) for k, s in shapes}
+    inbox = DeviceInbox(template, k_max=3, device=cuda)
+    for rnd in range(2):
+        inbox.reset()
+        ser = []
+        for j in range(3):
+            g = torch.Generator().manual_seed(100 * rnd + j)
+            ser.append(pickle.dumps({k: torch.randn(s, generator=g) for k, s in shapes}))
+        got = [inbox.land(_pinned(inbox, d), digest=True) for d in ser]
+        torch.cuda.synchronize()
+        for j, (d, g) in enumerate(zip(ser, got)):
+            ref = pickle.loads(d)
+            for key in ref:
+                assert torch.equal(g[key].cpu(), ref[key]), (rnd, j, key)
+            assert inbox.digest(j) == hashlib.sha256(d).digest()
+    assert len(inbox._pinned_free) <= 3  # buffers come back to the pool and are reused
+
+
+@pytest.mark.gpu
+def test_pinned_landing_strided_view_takes_staging_path(cuda):
+    """A transposed (non-dense) fp32 view cannot be a byte run: land() falls
+    back to the staging copy and the values still match pickle.loads."""
+    base = torch.randn(6, 4)
+    upd = {"w": base.t(), "b": torch.randn(4)}
+    data = pickle.dumps(upd)
+    template = {"w": torch.zeros(4, 6, device=cuda), "b": torch.zeros(4, device=cuda)}
+    inbox = DeviceInbox(template, k_max=1, device=cuda)
+    got = inbox.land(_pinned(inbox, data), 0)
+    torch.cuda.synchronize()
+    assert torch.equal(got["w"].cpu(), upd["w"]) and torch.equal(got["b"].cpu(), upd["b"])
+
+
+@pytest.mark.gpu
+def test_inbox_recv_into_pinned_and_land(cuda):
+    """DeviceInbox.recv: the reference framing (node/node.py:99-112) read into
+    a pinned buffer of the inbox; early close returns None."""
+    template = {name: torch.zeros(s, device=cuda) for name, s in MLP_SHAPES}
+    inbox = DeviceInbox(template, k_max=2, device=cuda)
+    data = pickle.dumps(mlp_update(7))
+    a, b = socket.socketpair()
+    th = threading.Thread(target=lambda: (a.sendall(len(data).to_bytes(4, "big") + data), a.close()))
+    th.start()
+    msg = inbox.recv(b)
+    th.join(10)
+    got = inbox.land(msg)
+    torch.cuda.synchronize()
+    ref = pickle.loads(data)
+    for key in ref:
+        assert_bits_equal(got[key].cpu().numpy(), ref[key].numpy(), what=key)
+    c, d = socket.socketpair()
+    c.sendall((100).to_bytes(4, "big") + b"xx")
+    c.close()
+    assert inbox.recv(d) is None
+    b.close()
+    d.close()
