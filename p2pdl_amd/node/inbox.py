@@ -486,12 +486,26 @@ class PinnedMessage:
 
     def __init__(self, capacity: int):
         self.buf = torch.empty(max(int(capacity), 1), dtype=torch.uint8, pin_memory=True)
+        self.start = 0
         self.nbytes = 0
+        self.root = self   # the pooled buffer a window lives in
         self.event = None  # the host-to-device copy that last read buf
         self.digest = None  # the SHA-256 future that reads buf
 
     def view(self) -> memoryview:
-        return memoryview(self.buf.numpy())[:self.nbytes]
+        return memoryview(self.buf.numpy())[self.start:self.start + self.nbytes]
+
+    def window(self, part: memoryview) -> "PinnedMessage":
+        """``part`` (a slice of ``view()``, e.g. the serialized update inside
+        the reference's envelope, node/node.py:133) as a message of its own
+        that shares this buffer: ``land`` reads it in place."""
+        base = self.buf.data_ptr()
+        at = np.frombuffer(part, dtype=np.uint8).ctypes.data - base if len(part) else self.start
+        if not (self.start <= at and at + len(part) <= self.start + self.nbytes):
+            raise ValueError("window outside the message")
+        w = PinnedMessage.__new__(PinnedMessage)
+        w.buf, w.start, w.nbytes, w.root, w.event, w.digest = self.buf, at, len(part), self.root, None, None
+        return w
 
     def wait_idle(self) -> None:
         if self.event is not None:
@@ -633,12 +647,12 @@ class DeviceInbox:
             serialized = pinned.view()
         fut = _hash_pool().submit(_sha256, serialized) if digest else None
         if pinned is not None:
-            pinned.digest = fut
+            pinned.root.digest = fut
         try:
             raw = ZeroCopyParser(serialized).parse()
         except BaseException:
             if pinned is not None:
-                self._release(pinned)
+                self._release(pinned.root)
             raise
         try:
             with self._lock:
@@ -657,7 +671,7 @@ class DeviceInbox:
                 return got if got is not None else self._land_locked(raw, k)
         finally:
             if pinned is not None:  # after the lock: the pool takes it
-                self._release(pinned)
+                self._release(pinned.root)
 
     def message_buffer(self, nbytes: int) -> PinnedMessage:
         """A pinned buffer for a message of ``nbytes`` (from the pool: one per
@@ -744,6 +758,26 @@ class DeviceInbox:
             slab_keys.append(key)
         return LandedUpdate(((key, out[key]) for key in raw), self, k, frozenset(slab_keys))
 
+    def open_envelope(self, msg: PinnedMessage) -> dict:
+        """The reference's message envelope (node/node.py:112: a pickled dict
+        -- 'type', 'addr', 'port', and for a model update the serialized
+        update under 'model', :133) parsed by the restricted machine (no
+        globals), with every bytes value a window of the pinned buffer
+        (``PinnedMessage.window``): ``land(command['model'])`` then reads the
+        update where it arrived.  ``pickle.UnpicklingError`` on anything else
+        (the buffer goes back to the pool)."""
+        try:
+            obj, pos = _run_pickle(msg.view(), 0, min_proto=2, resolve_global=_no_global)
+            if not isinstance(obj, dict) or pos != msg.nbytes:
+                raise pickle.UnpicklingError("an envelope must be one pickled dict")
+            return {k: (msg.window(v) if isinstance(v, memoryview) else v) for k, v in dict.items(obj)}
+        except pickle.UnpicklingError:
+            self._release(msg.root)
+            raise
+        except _MALFORMED as e:
+            self._release(msg.root)
+            raise pickle.UnpicklingError(f"malformed envelope: {type(e).__name__}: {e}") from e
+
     def _land_pinned_locked(self, msg: PinnedMessage, raw, k: int):
         """K5 device path: the message bytes in one DMA, then one landing
         kernel over a segment table (payload byte offset -> row offset).
@@ -752,7 +786,7 @@ class DeviceInbox:
         from .. import _native as N
         from .. import ops
 
-        base = msg.buf.data_ptr()
+        base = msg.buf.data_ptr() + msg.start
         row = self.slab[k]
         row_ptr = row.data_ptr()
         out = OrderedDict()
@@ -778,9 +812,9 @@ class DeviceInbox:
             d = self._dmsg[s]
             if d is None or d.numel() < msg.nbytes:
                 d = self._dmsg[s] = torch.empty(max(msg.nbytes, 1 << 20), dtype=torch.uint8, device=self.device)
-            d[:msg.nbytes].copy_(msg.buf[:msg.nbytes], non_blocking=True)
-            msg.event = torch.cuda.Event()
-            msg.event.record()
+            d[:msg.nbytes].copy_(msg.buf[msg.start:msg.start + msg.nbytes], non_blocking=True)
+            msg.root.event = torch.cuda.Event()
+            msg.root.event.record()
             if segs:
                 tab = np.zeros(len(segs), dtype=_LAND_SEG)
                 tab["src_off"] = [a for a, _, _ in segs]

@@ -681,3 +681,40 @@ def test_inbox_recv_into_pinned_and_land(cuda):
     assert inbox.recv(d) is None
     b.close()
     d.close()
+
+
+@pytest.mark.gpu
+def test_envelope_received_pinned_lands_in_place(cuda):
+    """The reference's own message (node/node.py:112,133: a pickled envelope
+    whose 'model' is the serialized update) received into a pinned buffer:
+    open_envelope hands 'model' out as a window of that buffer and land()
+    reads it in place; digest = SHA-256 of the serialized update (what the
+    echo signs, utils/broadcast.py:14)."""
+    import hashlib
+
+    template = {name: torch.zeros(s, device=cuda) for name, s in MLP_SHAPES}
+    inbox = DeviceInbox(template, k_max=2, device=cuda)
+    ser = pickle.dumps(mlp_update(11))
+    env = pickle.dumps({"type": "model_update", "model": ser, "addr": "127.0.0.1", "port": 5001})
+    a, b = socket.socketpair()
+    th = threading.Thread(target=lambda: (a.sendall(len(env).to_bytes(4, "big") + env), a.close()))
+    th.start()
+    msg = inbox.recv(b)
+    th.join(10)
+    b.close()
+    command = inbox.open_envelope(msg)
+    assert command["type"] == "model_update" and command["addr"] == "127.0.0.1" and command["port"] == 5001
+    assert bytes(command["model"].view()) == ser
+    got = inbox.land(command["model"], digest=True)
+    torch.cuda.synchronize()
+    ref = pickle.loads(ser)
+    for key in ref:
+        assert_bits_equal(got[key].cpu().numpy(), ref[key].numpy(), what=key)
+    assert inbox.digest(got.row) == hashlib.sha256(ser).digest()
+    # anything but a plain dict envelope is refused, and the buffer returns to the pool
+    bad = pickle.dumps({"type": "x", "f": collections.OrderedDict()})
+    m = inbox.message_buffer(len(bad))
+    m.buf[:len(bad)].copy_(torch.frombuffer(bytearray(bad), dtype=torch.uint8))
+    with pytest.raises(pickle.UnpicklingError):
+        inbox.open_envelope(m)
+    assert m in inbox._pinned_free
