@@ -718,3 +718,35 @@ def test_envelope_received_pinned_lands_in_place(cuda):
     with pytest.raises(pickle.UnpicklingError):
         inbox.open_envelope(m)
     assert m in inbox._pinned_free
+
+
+@pytest.mark.gpu
+def test_pinned_landing_concurrent_listeners(cuda):
+    """One listener thread per connection (node/node.py:89), each receiving
+    into its own pinned buffer from the pool and landing concurrently: every
+    update in its own row, bit-exact, buffers back in the pool."""
+    k = 8
+    template = {name: torch.zeros(s, device=cuda) for name, s in MLP_SHAPES}
+    inbox = DeviceInbox(template, k_max=k, device=cuda)
+    ser = [pickle.dumps(mlp_update(60 + j)) for j in range(k)]
+    got = [None] * k
+    barrier = threading.Barrier(k)
+
+    def worker(j):
+        barrier.wait()
+        for _ in range(3):  # reuse pooled buffers while others land
+            m = _pinned(inbox, ser[j])
+            got[j] = inbox.land(m, j)
+
+    ths = [threading.Thread(target=worker, args=(j,)) for j in range(k)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(60)
+    torch.cuda.synchronize()
+    assert len({got[j].row for j in range(k)}) == k
+    for j in range(k):
+        ref = pickle.loads(ser[j])
+        for key in ref:
+            assert_bits_equal(got[j][key].cpu().numpy(), ref[key].numpy(), what=f"update {j} {key}")
+    assert len(inbox._pinned_free) <= k
