@@ -140,60 +140,73 @@ def _run_pickle(mv: memoryview, pos: int, *, min_proto: int, resolve_global, per
     while pos < n:
         op = mv[pos]
         pos += 1
-        if op == 0x80:            # PROTO
-            if le(pos, 1) < min_proto:
+        if op == 0x94:          # MEMOIZE
+            memo[len(memo)] = stack[-1]
+        elif op == 0x4B:          # BININT1
+            stack.append(mv[pos])
+            pos += 1
+        elif op == 0x71:          # BINPUT
+            memo[mv[pos]] = stack[-1]
+            pos += 1
+        elif op == 0x58:          # BINUNICODE
+            k = le(pos, 4)
+            stack.append(str(blob(pos + 4, k), "utf-8"))
+            pos += 4 + k
+        elif op == 0x8C:          # SHORT_BINUNICODE
+            k = mv[pos]
+            stack.append(str(blob(pos + 1, k), "utf-8"))
+            pos += 1 + k
+        elif op == 0x52:          # REDUCE
+            args = stack.pop()
+            fn = stack[-1]
+            if not isinstance(fn, _Callable) or not isinstance(args, tuple):
+                raise pickle.UnpicklingError("REDUCE of something that is not an allowed global")
+            stack[-1] = fn(*args)
+        elif op == 0x28:          # MARK
+            stack.append(_MARK)
+        elif op == 0x68:          # BINGET
+            stack.append(memo[mv[pos]])
+            pos += 1
+        elif op == 0x85:          # TUPLE1
+            stack[-1] = (stack[-1],)
+        elif op == 0x74:          # TUPLE
+            items = pop_mark()  # rebinds `stack`: take the items first
+            stack.append(tuple(items))
+        elif op == 0x42:          # BINBYTES
+            k = le(pos, 4)
+            stack.append(blob(pos + 4, k))
+            pos += 4 + k
+        elif op == 0x89:          # NEWFALSE
+            stack.append(False)
+        elif op == 0x29:          # EMPTY_TUPLE
+            stack.append(())
+        elif op == 0x2E:          # STOP
+            return stack.pop(), pos
+        elif op == 0x80:            # PROTO
+            if mv[pos] < min_proto:
                 raise pickle.UnpicklingError(f"pickle protocol {mv[pos]} (< {min_proto}) is not accepted")
             pos += 1
         elif op == 0x95:          # FRAME (8-byte length; frames are inline)
             need(pos, 8)
             pos += 8
-        elif op == 0x2E:          # STOP
-            return stack.pop(), pos
-        elif op == 0x28:          # MARK
-            stack.append(_MARK)
         elif op == 0x7D:          # EMPTY_DICT
             stack.append({})
-        elif op == 0x29:          # EMPTY_TUPLE
-            stack.append(())
         elif op == 0x5D:          # EMPTY_LIST
             stack.append([])
-        elif op == 0x94:          # MEMOIZE
-            memo[len(memo)] = stack[-1]
-        elif op == 0x71:          # BINPUT
-            memo[le(pos, 1)] = stack[-1]
-            pos += 1
         elif op == 0x72:          # LONG_BINPUT
             memo[le(pos, 4)] = stack[-1]
             pos += 4
-        elif op == 0x68:          # BINGET
-            stack.append(memo[le(pos, 1)])
-            pos += 1
         elif op == 0x6A:          # LONG_BINGET
             stack.append(memo[le(pos, 4)])
             pos += 4
-        elif op == 0x8C:          # SHORT_BINUNICODE
-            k = le(pos, 1)
-            stack.append(str(blob(pos + 1, k), "utf-8"))
-            pos += 1 + k
-        elif op == 0x58:          # BINUNICODE
-            k = le(pos, 4)
-            stack.append(str(blob(pos + 4, k), "utf-8"))
-            pos += 4 + k
         elif op == 0x43:          # SHORT_BINBYTES
-            k = le(pos, 1)
+            k = mv[pos]
             stack.append(blob(pos + 1, k))
             pos += 1 + k
-        elif op == 0x42:          # BINBYTES
-            k = le(pos, 4)
-            stack.append(blob(pos + 4, k))
-            pos += 4 + k
         elif op == 0x8E:          # BINBYTES8
             k = le(pos, 8)
             stack.append(blob(pos + 8, k))
             pos += 8 + k
-        elif op == 0x4B:          # BININT1
-            stack.append(le(pos, 1))
-            pos += 1
         elif op == 0x4D:          # BININT2
             stack.append(le(pos, 2))
             pos += 2
@@ -201,17 +214,13 @@ def _run_pickle(mv: memoryview, pos: int, *, min_proto: int, resolve_global, per
             stack.append(int.from_bytes(blob(pos, 4), "little", signed=True))
             pos += 4
         elif op == 0x8A:          # LONG1
-            k = le(pos, 1)
+            k = mv[pos]
             stack.append(int.from_bytes(blob(pos + 1, k), "little", signed=True))
             pos += 1 + k
-        elif op == 0x89:          # NEWFALSE
-            stack.append(False)
         elif op == 0x88:          # NEWTRUE
             stack.append(True)
         elif op == 0x4E:          # NONE
             stack.append(None)
-        elif op == 0x85:          # TUPLE1
-            stack[-1] = (stack[-1],)
         elif op == 0x86:          # TUPLE2
             b = stack.pop()
             stack[-1] = (stack[-1], b)
@@ -219,9 +228,6 @@ def _run_pickle(mv: memoryview, pos: int, *, min_proto: int, resolve_global, per
             c = stack.pop()
             b = stack.pop()
             stack[-1] = (stack[-1], b, c)
-        elif op == 0x74:          # TUPLE
-            items = pop_mark()  # rebinds `stack`: take the items first
-            stack.append(tuple(items))
         elif op == 0x93:          # STACK_GLOBAL
             name = stack.pop()
             module = stack.pop()
@@ -239,12 +245,6 @@ def _run_pickle(mv: memoryview, pos: int, *, min_proto: int, resolve_global, per
             if persistent_load is None:
                 raise pickle.UnpicklingError("persistent ids are not accepted here")
             stack[-1] = persistent_load(stack[-1])
-        elif op == 0x52:          # REDUCE
-            args = stack.pop()
-            fn = stack[-1]
-            if not isinstance(fn, _Callable) or not isinstance(args, tuple):
-                raise pickle.UnpicklingError("REDUCE of something that is not an allowed global")
-            stack[-1] = fn(*args)
         elif op == 0x62:          # BUILD (OrderedDict metadata: set attributes)
             state = stack.pop()
             inst = stack[-1]
