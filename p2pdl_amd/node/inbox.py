@@ -35,6 +35,7 @@ this on torch-produced pickles of the reference's message shapes).
 """
 from __future__ import annotations
 
+import ctypes
 import hashlib
 import os
 import pickle
@@ -526,6 +527,15 @@ def _dense(rt: "RawTensor") -> bool:
     return True
 
 
+def _address(mv: memoryview) -> int:
+    """Host address of a (non-empty) buffer slice: through ctypes for the
+    writable pinned buffers (~0.3 us), numpy otherwise."""
+    try:
+        return ctypes.addressof(ctypes.c_char.from_buffer(mv))
+    except TypeError:
+        return np.frombuffer(mv, dtype=np.uint8).ctypes.data
+
+
 _LAND_TILE = 4096  # == P2P_LAND_TILE
 _LAND_SEG = np.dtype([("src_off", "<u8"), ("dst", "<u8"), ("n", "<i8"), ("tile_begin", "<i8")])
 
@@ -612,6 +622,7 @@ class DeviceInbox:
         self._stage = [torch.empty(self.row, dtype=torch.float32, pin_memory=True) for _ in range(2)]
         self._events = [None, None]
         self._dmsg = [None, None]  # device copies of pinned messages (landing kernel input)
+        self._views = [{} for _ in range(self.k_max)]  # row k: {key: slab view}
         self._pinned_free = []     # PinnedMessage pool
         self._digests = {}
         self.count = 0
@@ -753,8 +764,7 @@ class DeviceInbox:
         for key in raw:
             if key in out:
                 continue
-            off, shape, n = self.layout[key]
-            out[key] = row[off:off + n].view(shape)
+            out[key] = self._row_view(k, key)
             slab_keys.append(key)
         return LandedUpdate(((key, out[key]) for key in raw), self, k, frozenset(slab_keys))
 
@@ -800,7 +810,7 @@ class DeviceInbox:
                 if not _dense(rt):
                     return None
                 if n:
-                    src = np.frombuffer(rt.storage.data, dtype=np.uint8).ctypes.data - base + 4 * rt.offset
+                    src = _address(rt.storage.data) - base + 4 * rt.offset
                     segs.append((src, row_ptr + 4 * off, n))
             else:  # not part of the fp32 slab: a small tensor of its own
                 out[key] = torch.from_numpy(np.array(rt.array())).to(self.device)
@@ -834,10 +844,20 @@ class DeviceInbox:
         for key in raw:
             if key in out:
                 continue
-            off, shape, n = self.layout[key]
-            out[key] = row[off:off + n].view(shape)
+            out[key] = self._row_view(k, key)
             slab_keys.append(key)
         return LandedUpdate(((key, out[key]) for key in raw), self, k, frozenset(slab_keys))
+
+    def _row_view(self, k: int, key):
+        """slab[k, off : off + n].view(shape) for a template key, built once
+        per (row, key): the slab is never reallocated, so the view is the
+        same every round (62 tensor slices per ResNet-18 update otherwise)."""
+        views = self._views[k]
+        v = views.get(key)
+        if v is None:
+            off, shape, n = self.layout[key]
+            v = views[key] = self.slab[k, off:off + n].view(shape)
+        return v
 
     def view(self, k: int) -> LandedUpdate:
         """Row k as a landed update holding every fp32 key of the template

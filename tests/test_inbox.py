@@ -750,3 +750,20 @@ def test_pinned_landing_concurrent_listeners(cuda):
         for key in ref:
             assert_bits_equal(got[j][key].cpu().numpy(), ref[key].numpy(), what=f"update {j} {key}")
     assert len(inbox._pinned_free) <= k
+
+
+def test_dense_views_and_buffer_addresses():
+    """Host helpers of the pinned landing path: which fp32 views can land as
+    one byte run, and the address of a payload slice (writable or not)."""
+    from p2pdl_amd.node.inbox import RawStorage, RawTensor, _address, _dense
+
+    st = RawStorage(np.float32, 24, memoryview(bytearray(96)), "cpu")
+    assert _dense(RawTensor(st, 0, (4, 6), (6, 1)))
+    assert _dense(RawTensor(st, 3, (1, 6), (99, 1)))   # a size-1 dim may carry any stride
+    assert _dense(RawTensor(st, 0, (), ()))
+    assert not _dense(RawTensor(st, 0, (6, 4), (1, 6)))  # transposed
+    assert not _dense(RawTensor(st, 0, (3,), (2,)))       # strided
+    a = np.zeros(64, np.uint8)
+    assert _address(memoryview(a)[5:9]) == a.ctypes.data + 5
+    b = bytes(64)
+    assert _address(memoryview(b)[7:9]) == np.frombuffer(b, np.uint8).ctypes.data + 7
