@@ -144,7 +144,8 @@ def parallelism(c: Ctx) -> str:
     if c.world == 1:
         return "single GPU"
     via = "RCCL over xGMI" if c.backend == "nccl" else f"{c.backend} (rehearsal, ranks share one GPU)"
-    return f"coord-shard x{c.world}, all_gather_into_tensor via {via}"
+    return (f"coord-shard x{dist.get_world_size()} (process group world size, backend "
+            f"{dist.get_backend()}), all_gather_into_tensor via {via}")
 
 
 def oracle_expect(rule, K, m, seed, chunk=0, nranks=1, rank=0):
@@ -893,15 +894,63 @@ def compact_sub(rec: dict) -> dict:
     return out
 
 
+def launch_plan(gpus: int, env, visible: int, backend: str):
+    """How this process runs ``--gpus N`` (no GPU is touched here):
+      ("spawn", N)  WORLD_SIZE unset and N > 1: start N ranks as children
+                    (torch.distributed.run, one process per GPU) and relay;
+      ("rank", W)   inside a launcher (WORLD_SIZE = W) or N == 1: run as a rank.
+    A launcher world that differs from --gpus, or an RCCL world larger than
+    the visible GPUs, is an error (SystemExit), never a silent 1-GPU line."""
+    if gpus < 1:
+        raise SystemExit(f"bench: --gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        world = gpus
+        if gpus == 1:
+            return "rank", 1
+    else:
+        world = int(ws)
+        if world != gpus:
+            raise SystemExit(f"bench: WORLD_SIZE={world} from the launcher but --gpus {gpus}")
+    if world > 1 and backend == "nccl" and visible < world:
+        raise SystemExit(f"bench: --gpus {world} over RCCL needs {world} GPUs, {visible} visible "
+                         f"(P2P_DIST_BACKEND=gloo rehearses several ranks on one GPU)")
+    return ("spawn", world) if ws is None else ("rank", world)
+
+
+def spawn_command(gpus: int, port: int, argv) -> list:
+    """The child launch of ``--gpus N`` without an outer launcher: one rank per
+    GPU on this node, rendezvous on 127.0.0.1 (the driver's own N > 1 form)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # P2P_DIST_BACKEND=gloo rehearses N>1 on a single GPU (ranks share cuda:0);
     # the driver's multi-GPU runs use nccl (= RCCL over xGMI), one GPU per rank.
     backend = os.environ.get("P2P_DIST_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
+    visible = torch.cuda.device_count()  # does not initialise the GPU on this image
+    mode, world = launch_plan(args.gpus, os.environ, visible, backend)
+    if mode == "spawn":
+        # this parent never touches the GPU: the ranks are its children and
+        # rank 0's JSON line reaches our stdout directly
+        import subprocess
+
+        cmd = spawn_command(world, _free_port(), sys.argv[1:])
+        log(f"bench: --gpus {world}: launching {world} ranks ({backend}): {' '.join(cmd)}")
+        sys.exit(subprocess.call(cmd))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, visible)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -909,6 +958,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, expected {world}")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     c = Ctx(world=world, rank=rank, dev=dev, backend=backend)

@@ -88,6 +88,7 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
     if table is not None:
         ws_c = [w if w.is_contiguous() else w.contiguous() for w in ws]
         ops.aggregate_ptr_table_(ws_c, table, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac)
+        _mark_rows_consumed(received)
         for w, wc in zip(ws, ws_c):
             if wc is not w:
                 w.copy_(wc)
@@ -112,6 +113,7 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
     # updates the model, exactly like the reference's `+=` at :38.
     ws_c = [w if w.is_contiguous() else w.contiguous() for w in ws]
     ops.aggregate_segments_(ws_c, peer_lists, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac)
+    _mark_rows_consumed(received)
     for w, wc in zip(ws, ws_c):
         if wc is not w:
             w.copy_(wc)
@@ -188,9 +190,24 @@ def _slab_fast_path(state, keys, received, rule, lr, trim_frac) -> bool:
         ws.append(t)
         offsets.append(off)
     inbox.order_after_landing()  # land()'s row copies ran on the listener thread's stream
-    ops.aggregate_slab_rows_(ws, inbox.slab, [rm["model"].row for rm in received], offsets, rule,
-                             lr=lr, trim_frac=trim_frac)
+    rows = [rm["model"].row for rm in received]
+    ops.aggregate_slab_rows_(ws, inbox.slab, rows, offsets, rule, lr=lr, trim_frac=trim_frac)
+    inbox.slab_consumed()  # the next round's land() into these rows waits for this kernel
     return True
+
+
+def _mark_rows_consumed(received) -> None:
+    """General path over landed updates (e.g. mixed with plain dicts): each
+    inbox learns that the launch just issued reads its rows."""
+    from ..node.inbox import LandedUpdate
+
+    inboxes = {}
+    for rm in received:
+        u = rm.get("model") if isinstance(rm, dict) else None
+        if isinstance(u, LandedUpdate):
+            inboxes[id(u.inbox)] = u.inbox
+    for inbox in inboxes.values():
+        inbox.slab_consumed()
 
 
 _PINNED = {}  # (device, numel) -> pinned host staging buffer, reused across rounds

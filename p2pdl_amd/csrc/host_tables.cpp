@@ -17,13 +17,17 @@
 // Returns 0 with out filled when every tensor is fp32, contiguous, on
 // `device` with numels[l] elements; 1 (out partially written, nothing
 // raised) when some tensor needs the Python path's exact diagnosis or
-// widening; raises what the reference's lookups raise (KeyError, TypeError).
+// widening (a sparse or other non-strided tensor included: its layout is
+// checked before any strided-only getter); raises what the reference's
+// lookups raise (KeyError, TypeError), and RuntimeError if an ATen getter
+// throws -- no C++ exception unwinds through this CPython function.
 #include <Python.h>
 
 #include <ATen/core/Tensor.h>
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
+#include <exception>
 #include <vector>
 
 namespace {
@@ -45,16 +49,25 @@ PyObject* get_item(PyObject* mapping, PyObject* key) {
   return PyObject_GetItem(mapping, key);
 }
 
-PyObject* gather_peer_table(PyObject*, PyObject* args) {
-  PyObject *received, *keys, *numels_obj;
-  int device;
-  Py_buffer out;
-  if (!PyArg_ParseTuple(args, "O!O!O!iw*", &PyList_Type, &received, &PyList_Type, &keys, &PyList_Type,
-                        &numels_obj, &device, &out))
-    return nullptr;
+// Py_buffer released on every exit path (the C++ exception path included).
+struct BufferGuard {
+  Py_buffer* b;
+  ~BufferGuard() { PyBuffer_Release(b); }
+};
+
+// status 0: x is a dense fp32 tensor on `device` with n elements.  The layout
+// is checked before any getter that only strided tensors implement
+// (is_contiguous throws c10::Error on a sparse tensor).
+int vouch(const at::Tensor& x, int device, int64_t n) {
+  if (x.layout() != at::kStrided || x.scalar_type() != at::kFloat || !x.is_cuda() || x.get_device() != device)
+    return 1;
+  return (x.numel() == n && x.is_contiguous()) ? 0 : 1;
+}
+
+PyObject* gather_peer_table_impl(PyObject* received, PyObject* keys, PyObject* numels_obj, int device,
+                                 Py_buffer* out) {
   const Py_ssize_t K = PyList_GET_SIZE(received), L = PyList_GET_SIZE(keys);
-  if (out.len < static_cast<Py_ssize_t>(sizeof(uint64_t)) * L * K || PyList_GET_SIZE(numels_obj) != L) {
-    PyBuffer_Release(&out);
+  if (out->len < static_cast<Py_ssize_t>(sizeof(uint64_t)) * L * K || PyList_GET_SIZE(numels_obj) != L) {
     PyErr_SetString(PyExc_ValueError, "gather_peer_table: buffer / numels do not match L x K");
     return nullptr;
   }
@@ -62,23 +75,16 @@ PyObject* gather_peer_table(PyObject*, PyObject* args) {
   std::vector<int64_t> numels(static_cast<size_t>(L));
   for (Py_ssize_t l = 0; l < L; ++l) {
     numels[l] = PyLong_AsLongLong(PyList_GET_ITEM(numels_obj, l));
-    if (numels[l] == -1 && PyErr_Occurred()) {
-      PyBuffer_Release(&out);
-      return nullptr;
-    }
+    if (numels[l] == -1 && PyErr_Occurred()) return nullptr;
   }
-  uint64_t* table = static_cast<uint64_t*>(out.buf);
+  uint64_t* table = static_cast<uint64_t*>(out->buf);
   for (Py_ssize_t j = 0; j < K && status == 0; ++j) {
     PyObject* model = get_item(PyList_GET_ITEM(received, j), g_model_key);
-    if (!model) {
-      PyBuffer_Release(&out);
-      return nullptr;
-    }
+    if (!model) return nullptr;
     for (Py_ssize_t l = 0; l < L; ++l) {
       PyObject* t = get_item(model, PyList_GET_ITEM(keys, l));
       if (!t) {
         Py_DECREF(model);
-        PyBuffer_Release(&out);
         return nullptr;
       }
       if (!THPVariable_Check(t)) {
@@ -86,20 +92,37 @@ PyObject* gather_peer_table(PyObject*, PyObject* args) {
         status = 1;  // not a tensor: the Python path reports it the reference's way
         break;
       }
-      const at::Tensor& x = THPVariable_Unpack(t);
-      if (x.scalar_type() != at::kFloat || !x.is_cuda() || x.get_device() != device || !x.is_contiguous() ||
-          x.numel() != numels[l]) {
+      int bad;
+      try {
+        const at::Tensor& x = THPVariable_Unpack(t);
+        bad = vouch(x, device, numels[l]);
+        if (!bad) table[l * K + j] = reinterpret_cast<uint64_t>(x.data_ptr());
+      } catch (const std::exception& e) {  // an ATen getter threw: a Python error, never std::terminate
         Py_DECREF(t);
+        Py_DECREF(model);
+        PyErr_Format(PyExc_RuntimeError, "gather_peer_table: %s", e.what());
+        return nullptr;
+      }
+      Py_DECREF(t);
+      if (bad) {
         status = 1;
         break;
       }
-      table[l * K + j] = reinterpret_cast<uint64_t>(x.data_ptr());
-      Py_DECREF(t);
     }
     Py_DECREF(model);
   }
-  PyBuffer_Release(&out);
   return PyLong_FromLong(status);
+}
+
+PyObject* gather_peer_table(PyObject*, PyObject* args) {
+  PyObject *received, *keys, *numels_obj;
+  int device;
+  Py_buffer out;
+  if (!PyArg_ParseTuple(args, "O!O!O!iw*", &PyList_Type, &received, &PyList_Type, &keys, &PyList_Type,
+                        &numels_obj, &device, &out))
+    return nullptr;
+  BufferGuard guard{&out};
+  return gather_peer_table_impl(received, keys, numels_obj, device, &out);
 }
 
 PyMethodDef methods[] = {

@@ -36,7 +36,6 @@ this on torch-produced pickles of the reference's message shapes).
 from __future__ import annotations
 
 import ctypes
-import hashlib
 import os
 import pickle
 import struct
@@ -46,6 +45,8 @@ from dataclasses import dataclass
 
 import numpy as np
 import torch
+
+from ..utils import digests
 
 # torch legacy serialization (torch/serialization.py _legacy_save): magic
 # number pickle, protocol-version pickle, sys_info pickle, the object pickle
@@ -463,6 +464,9 @@ def recv_exact_into(conn, buf: memoryview) -> int:
     return got
 
 
+_RECV_STEP = 64 << 20  # pageable receive grows in steps of this size (bytes arrive first)
+
+
 def recv_message(conn) -> bytearray | None:
     """One length-prefixed message (reference node/node.py:99-112 framing:
     4-byte big-endian length, then the pickle), received linearly.  Returns
@@ -470,43 +474,47 @@ def recv_message(conn) -> bytearray | None:
     hdr = bytearray(4)
     if recv_exact_into(conn, memoryview(hdr)) != 4:
         return None
-    n = int.from_bytes(hdr, "big")
-    data = bytearray(n)
-    if recv_exact_into(conn, memoryview(data)) != n:
-        return None
-    return data
+    return recv_body(conn, int.from_bytes(hdr, "big"))
 
 
-class PinnedMessage:
-    """One received message in page-locked host memory (``DeviceInbox.recv``
-    / ``message_buffer``).  ``DeviceInbox.land`` moves it to the device in ONE
-    DMA, as bytes, and the landing kernel (csrc/land.hip) places its fp32
-    payloads in the slab row: the host never copies a payload byte.  Handed
-    back to the inbox's pool by ``land`` (reused once that DMA -- and the
-    digest, if one was asked for -- has finished)."""
+def recv_body(conn, n: int) -> bytearray | None:
+    """The n message bytes after the length prefix, in pageable memory that
+    grows as bytes arrive (from 64 MiB, doubling), like the reference's
+    buffer: a bogus length claims no memory up front.  None on early close."""
+    data = bytearray(min(n, _RECV_STEP))
+    got = 0
+    while True:
+        got += recv_exact_into(conn, memoryview(data)[got:])
+        if got < len(data):
+            return None
+        if got == n:
+            return data
+        data += bytes(min(len(data), n - len(data)))
 
-    def __init__(self, capacity: int):
-        self.buf = torch.empty(max(int(capacity), 1), dtype=torch.uint8, pin_memory=True)
-        self.start = 0
-        self.nbytes = 0
-        self.root = self   # the pooled buffer a window lives in
-        self.event = None  # the host-to-device copy that last read buf
-        self.digest = None  # the SHA-256 future that reads buf
 
-    def view(self) -> memoryview:
-        return memoryview(self.buf.numpy())[self.start:self.start + self.nbytes]
+_REF_LOCK = threading.Lock()
 
-    def window(self, part: memoryview) -> "PinnedMessage":
-        """``part`` (a slice of ``view()``, e.g. the serialized update inside
-        the reference's envelope, node/node.py:133) as a message of its own
-        that shares this buffer: ``land`` reads it in place."""
-        base = self.buf.data_ptr()
-        at = np.frombuffer(part, dtype=np.uint8).ctypes.data - base if len(part) else self.start
-        if not (self.start <= at and at + len(part) <= self.start + self.nbytes):
-            raise ValueError("window outside the message")
-        w = PinnedMessage.__new__(PinnedMessage)
-        w.buf, w.start, w.nbytes, w.root, w.event, w.digest = self.buf, at, len(part), self.root, None, None
-        return w
+
+def _pinned_bytes(n: int) -> torch.Tensor:
+    return torch.empty(n, dtype=torch.uint8, pin_memory=True)
+
+
+class _PinnedBuffer:
+    """A page-locked host buffer of the inbox's pool.  ``refs`` counts the
+    live ``PinnedMessage`` handles on it (the received message and the
+    windows cut from it); at zero it goes back to the pool, and it is handed
+    out again only after the last DMA and digest that read it are done."""
+
+    def __init__(self, capacity: int, pool):
+        self.buf = _pinned_bytes(max(int(capacity), 1))
+        self.pool = pool      # the DeviceInbox whose pool it returns to
+        self.refs = 0
+        self.event = None     # the host-to-device copy that last read buf
+        self.digest = None    # the SHA-256 future that reads buf
+
+    @property
+    def capacity(self) -> int:
+        return self.buf.numel()
 
     def wait_idle(self) -> None:
         if self.event is not None:
@@ -515,6 +523,91 @@ class PinnedMessage:
         if self.digest is not None:
             self.digest.result()
             self.digest = None
+
+
+class PinnedMessage:
+    """A handle on a received message in page-locked host memory
+    (``DeviceInbox.recv`` / ``message_buffer``), or on a window of one
+    (``window``, e.g. the serialized update inside the reference's envelope,
+    node/node.py:133).  ``DeviceInbox.land`` moves it to the device in ONE
+    DMA, as bytes, and the landing kernel (csrc/land.hip) places its fp32
+    payloads in the slab row: the host never copies a payload byte.
+
+    The bytes stay valid, and the buffer stays out of the pool, while ANY
+    handle on it is alive: ``release()`` (or garbage collection of the
+    handle) gives the handle up, and when the last one goes the buffer
+    returns to the inbox's pool.  ``land`` does not release: a listener can
+    still read ``view()`` (the echo's bytes, utils/broadcast.py:14,23) after
+    landing.  Pickled, a handle is its bytes (the echo envelope carries them,
+    utils/broadcast.py:18-24)."""
+
+    def __init__(self, root: _PinnedBuffer, start: int, nbytes: int):
+        self.root, self.start, self.nbytes = root, int(start), int(nbytes)
+        self.buf = root.buf
+        with _REF_LOCK:
+            root.refs += 1
+        self._held = True
+
+    def view(self) -> memoryview:
+        if not self._held:
+            raise ValueError("the message was released (its buffer may hold another message)")
+        return memoryview(self.buf.numpy())[self.start:self.start + self.nbytes]
+
+    def __len__(self) -> int:
+        return self.nbytes
+
+    def __bytes__(self) -> bytes:
+        return bytes(self.view())
+
+    def __reduce__(self):
+        return (bytes, (bytes(self.view()),))
+
+    def window(self, part: memoryview) -> "PinnedMessage":
+        """``part`` (a slice of ``view()``) as a message of its own that shares
+        this buffer (and holds it): ``land`` reads it in place."""
+        base = self.buf.data_ptr()
+        at = np.frombuffer(part, dtype=np.uint8).ctypes.data - base if len(part) else self.start
+        if not (self.start <= at and at + len(part) <= self.start + self.nbytes):
+            raise ValueError("window outside the message")
+        return PinnedMessage(self.root, at, len(part))
+
+    def release(self) -> None:
+        """Give this handle up (idempotent)."""
+        with _REF_LOCK:
+            if not self._held:
+                return
+            self._held = False
+            self.root.refs -= 1
+            last = self.root.refs == 0
+        if last and self.root.pool is not None:
+            self.root.pool._release(self.root)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.release()
+        return False
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:  # interpreter shutdown
+            pass
+
+
+def _detached(v):
+    """A restricted-machine value with every byte string (a memoryview of
+    the receive buffer) copied out as bytes, at any depth."""
+    if isinstance(v, memoryview):
+        return bytes(v)
+    if isinstance(v, list):
+        return [_detached(x) for x in v]
+    if isinstance(v, tuple):
+        return tuple(_detached(x) for x in v)
+    if isinstance(v, dict):
+        return {_detached(a): _detached(b) for a, b in dict.items(v)}
+    return v
 
 
 def _dense(rt: "RawTensor") -> bool:
@@ -604,7 +697,8 @@ class DeviceInbox:
     k; ``reset()`` starts a new round.  Non-fp32 entries (e.g. int64
     counters) are materialised as ordinary small device tensors."""
 
-    def __init__(self, template: dict, k_max: int, device=None):
+    def __init__(self, template: dict, k_max: int, device=None, max_message_bytes: int | None = None,
+                 pool_bytes: int | None = None):
         self.device = torch.device(device) if device is not None else next(
             (t.device for t in template.values() if t.is_cuda), torch.device("cuda", torch.cuda.current_device()))
         self.layout = OrderedDict()
@@ -623,7 +717,17 @@ class DeviceInbox:
         self._events = [None, None]
         self._dmsg = [None, None]  # device copies of pinned messages (landing kernel input)
         self._views = [{} for _ in range(self.k_max)]  # row k: {key: slab view}
-        self._pinned_free = []     # PinnedMessage pool
+        # A message of up to max_message_bytes is received into pinned memory
+        # (default: the template's payload plus the pickle framing -- about 325
+        # B per tensor, SURVEY.md §3D -- and 1 MiB of envelope / extra keys);
+        # a longer one into pageable memory.  The pool of free pinned buffers
+        # holds at most pool_bytes (default: two per row of the slab).
+        extra = sum(t.numel() * t.element_size() for t in template.values() if t.dtype != torch.float32)
+        self.max_message_bytes = int(max_message_bytes if max_message_bytes is not None else
+                                     4 * self.row + extra + 1024 * len(template) + (1 << 20))
+        self.pool_bytes = int(pool_bytes if pool_bytes is not None else 2 * self.k_max * self.max_message_bytes)
+        self._pinned_free = []     # _PinnedBuffer pool
+        self._consumers = {}       # stream handle -> event after its last kernel over the slab
         self._digests = {}
         self.count = 0
         # land() is called from the listener threads (one per connection,
@@ -649,71 +753,98 @@ class DeviceInbox:
         digest=True also starts SHA-256 of the serialized bytes -- what the
         tester signs in its echo (node/node.py:144 -> utils/crypto.py:54-57)
         -- on a hashing thread, overlapped with the parse, the staging copy
-        and the DMA of this update and the next; ``digest(k)`` returns it.
-        The buffer must not change until then.  (Host SHA-NI: one message is
-        one serial chain, ~1.4 GB/s on a host core vs ~35 MB/s on one GPU
-        lane -- DESIGN.md §3 K3.)"""
+        and the DMA of this update and the next; ``digest(k)`` returns it,
+        and so does the process's digest cache (utils/digests.py) for this
+        same object: the echo's ``sign_data(key, serialized)`` (reference
+        utils/broadcast.py:14, unchanged) reuses it.  The buffer must not
+        change until then.  (Host SHA-NI: one message is one serial chain,
+        ~2.4 GB/s on a host core vs ~33 MB/s on one GPU lane -- DESIGN.md §3
+        K3.)  Landing does not release a ``PinnedMessage``: its bytes stay
+        valid until every handle on its buffer is released."""
         pinned = serialized if isinstance(serialized, PinnedMessage) else None
         if pinned is not None:
             serialized = pinned.view()
-        fut = _hash_pool().submit(_sha256, serialized) if digest else None
-        if pinned is not None:
-            pinned.root.digest = fut
-        try:
-            raw = ZeroCopyParser(serialized).parse()
-        except BaseException:
-            if pinned is not None:
-                self._release(pinned.root)
-            raise
-        try:
-            with self._lock:
-                if k is None:
-                    k = self.count
-                if not 0 <= k < self.k_max:
-                    raise IndexError(f"slab row {k} out of range (k_max={self.k_max})")
-                self.count = max(self.count, k + 1)
-                if fut is not None:
-                    self._digests[k] = fut
-                else:  # a digest of the row's previous bytes must not outlive them
-                    self._digests.pop(k, None)
-                if pinned is None:
-                    return self._land_locked(raw, k)
-                got = self._land_pinned_locked(pinned, raw, k)
-                return got if got is not None else self._land_locked(raw, k)
-        finally:
-            if pinned is not None:  # after the lock: the pool takes it
-                self._release(pinned.root)
+        # SHA-256 of the bytes on a hashing thread, registered in the process's
+        # digest cache under this very object: sign_data / verify_signature of
+        # it (utils/crypto.py) then pick it up instead of hashing again
+        fut = digests.digest_async(pinned if pinned is not None else serialized) if digest else None
+        if pinned is not None and fut is not None:
+            pinned.root.digest = fut  # the pool hands the buffer out again only after it
+        raw = ZeroCopyParser(serialized).parse()
+        with self._lock:
+            if k is None:
+                k = self.count
+            if not 0 <= k < self.k_max:
+                raise IndexError(f"slab row {k} out of range (k_max={self.k_max})")
+            self.count = max(self.count, k + 1)
+            if fut is not None:
+                self._digests[k] = fut
+            else:  # a digest of the row's previous bytes must not outlive them
+                self._digests.pop(k, None)
+            if pinned is None:
+                return self._land_locked(raw, k)
+            got = self._land_pinned_locked(pinned, raw, k)
+            return got if got is not None else self._land_locked(raw, k)
 
     def message_buffer(self, nbytes: int) -> PinnedMessage:
-        """A pinned buffer for a message of ``nbytes`` (from the pool: one per
-        message in flight; ``land`` returns it)."""
+        """A pinned buffer for a message of ``nbytes`` (the smallest free one
+        of the pool that fits, or a new one), as a handle; the buffer returns
+        to the pool when the handle and every window of it are released."""
+        nbytes = int(nbytes)
         with self._lock:
-            m = next((p for p in self._pinned_free if p.buf.numel() >= nbytes), None)
-            if m is not None:
-                self._pinned_free.remove(m)
-        if m is None:
-            m = PinnedMessage(nbytes)
-        m.wait_idle()
-        m.nbytes = int(nbytes)
-        return m
+            fits = [p for p in self._pinned_free if p.capacity >= nbytes]
+            root = min(fits, key=lambda p: p.capacity) if fits else None
+            if root is not None:
+                self._pinned_free.remove(root)
+        if root is None:
+            root = _PinnedBuffer(nbytes, self)
+        root.wait_idle()
+        return PinnedMessage(root, 0, nbytes)
 
-    def _release(self, m: PinnedMessage) -> None:
+    def _release(self, root: _PinnedBuffer) -> None:
+        """A buffer with no live handle: back to the pool while the pool holds
+        at most pool_bytes, freed otherwise."""
         with self._lock:
-            if m not in self._pinned_free:
-                self._pinned_free.append(m)
+            if any(p is root for p in self._pinned_free):
+                return
+            if sum(p.capacity for p in self._pinned_free) + root.capacity <= self.pool_bytes:
+                self._pinned_free.append(root)
 
-    def recv(self, conn) -> PinnedMessage | None:
+    def recv(self, conn):
         """``recv_message`` into a pinned buffer of this inbox: the 4-byte
-        big-endian length (node/node.py:99-112 framing), then the message.
+        big-endian length (node/node.py:99-112 framing), then the message, as
+        a ``PinnedMessage``.  A message longer than ``max_message_bytes``
+        arrives in pageable memory instead (a ``bytearray`` that grows as
+        bytes arrive), so a peer's length field cannot pin host memory.
         None if the peer closed early (the buffer goes back to the pool)."""
         hdr = bytearray(4)
         if recv_exact_into(conn, memoryview(hdr)) != 4:
             return None
-        m = self.message_buffer(int.from_bytes(hdr, "big"))
+        n = int.from_bytes(hdr, "big")
+        if n > self.max_message_bytes:
+            return recv_body(conn, n)
+        m = self.message_buffer(n)
         if recv_exact_into(conn, m.view()) != m.nbytes:
-            self._release(m)
+            m.release()
             return None
         return m
+
+    def slab_consumed(self, stream=None) -> None:
+        """Record that a kernel just issued on ``stream`` (default: the current
+        stream of the slab's device) reads slab rows: every later ``land``
+        makes its own stream wait for that kernel before it overwrites a row
+        (aggregation.py calls this after each launch over landed updates).
+        One event per consuming stream, re-recorded -- no allocation per call."""
+        stream = stream or torch.cuda.current_stream(self.device)
+        with self._lock:
+            ev = self._consumers.get(stream.cuda_stream)
+            if ev is None:
+                ev = self._consumers[stream.cuda_stream] = torch.cuda.Event()
+            ev.record(stream)
+
+    def _wait_rows_free(self, stream) -> None:
+        for ev in self._consumers.values():  # under self._lock
+            stream.wait_event(ev)
 
     def order_after_landing(self, stream=None) -> None:
         """Make ``stream`` (default: the current stream of the slab's device)
@@ -756,6 +887,7 @@ class DeviceInbox:
                 out[key] = torch.from_numpy(np.array(rt.array())).to(self.device)
         _copy_all(jobs)
         with torch.cuda.device(self.device):
+            self._wait_rows_free(torch.cuda.current_stream())
             row.copy_(self._stage[s], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
@@ -768,25 +900,36 @@ class DeviceInbox:
             slab_keys.append(key)
         return LandedUpdate(((key, out[key]) for key in raw), self, k, frozenset(slab_keys))
 
-    def open_envelope(self, msg: PinnedMessage) -> dict:
-        """The reference's message envelope (node/node.py:112: a pickled dict
-        -- 'type', 'addr', 'port', and for a model update the serialized
-        update under 'model', :133) parsed by the restricted machine (no
-        globals), with every bytes value a window of the pinned buffer
-        (``PinnedMessage.window``): ``land(command['model'])`` then reads the
-        update where it arrived.  ``pickle.UnpicklingError`` on anything else
-        (the buffer goes back to the pool)."""
+    def open_envelope(self, msg) -> dict:
+        """The reference's message envelope decoded (replaces pickle.loads at
+        node/node.py:112) from what ``recv`` returned.
+
+        A plain envelope of a ``model_update`` (a pickled dict: 'type', 'addr',
+        'port' and the serialized update under 'model', :130-135) is parsed by
+        the restricted machine (no globals) and 'model' comes back as a
+        ``PinnedMessage`` window of the receive buffer, so ``land`` reads the
+        update where it arrived; every other bytes value is real ``bytes``.
+        Any other message -- 'global_model_update' carries a state_dict of
+        tensors (aggregation.py:70), 'echo' / 'ready' / 'sup' carry
+        signatures and whole updates as bytes -- is decoded as the reference
+        decodes it, with every value a plain object.  The handle ``msg`` is
+        consumed: its buffer returns to the pool once no window of it is
+        alive (at once when none escapes)."""
+        if not isinstance(msg, PinnedMessage):  # pageable (over the pinned cap)
+            return pickle.loads(msg)
         try:
-            obj, pos = _run_pickle(msg.view(), 0, min_proto=2, resolve_global=_no_global)
-            if not isinstance(obj, dict) or pos != msg.nbytes:
-                raise pickle.UnpicklingError("an envelope must be one pickled dict")
-            return {k: (msg.window(v) if isinstance(v, memoryview) else v) for k, v in dict.items(obj)}
-        except pickle.UnpicklingError:
-            self._release(msg.root)
-            raise
-        except _MALFORMED as e:
-            self._release(msg.root)
-            raise pickle.UnpicklingError(f"malformed envelope: {type(e).__name__}: {e}") from e
+            mv = msg.view()
+            try:
+                obj, pos = _run_pickle(mv, 0, min_proto=2, resolve_global=_no_global)
+                plain = isinstance(obj, dict) and pos == msg.nbytes
+            except (pickle.UnpicklingError, *_MALFORMED):
+                plain = False
+            if not (plain and dict.get(obj, "type") == "model_update" and isinstance(dict.get(obj, "model"),
+                                                                                 memoryview)):
+                return pickle.loads(mv)  # the reference's own decode of the envelope
+            return {k: (msg.window(v) if k == "model" else _detached(v)) for k, v in dict.items(obj)}
+        finally:
+            msg.release()
 
     def _land_pinned_locked(self, msg: PinnedMessage, raw, k: int):
         """K5 device path: the message bytes in one DMA, then one landing
@@ -811,6 +954,13 @@ class DeviceInbox:
                     return None
                 if n:
                     src = _address(rt.storage.data) - base + 4 * rt.offset
+                    # the parser already bounds every view by its storage and
+                    # every storage by the message; a layout that still points
+                    # outside the message fails here, loudly, instead of landing
+                    # the kernel's zero fill
+                    if src < 0 or src + 4 * n > msg.nbytes:
+                        raise pickle.UnpicklingError(f"update key {key}: payload [{src}, {src + 4 * n}) "
+                                                     f"outside the {msg.nbytes}-byte message")
                     segs.append((src, row_ptr + 4 * off, n))
             else:  # not part of the fp32 slab: a small tensor of its own
                 out[key] = torch.from_numpy(np.array(rt.array())).to(self.device)
@@ -819,6 +969,7 @@ class DeviceInbox:
             stream = torch.cuda.current_stream()
             if self._events[s] is not None:
                 stream.wait_event(self._events[s])  # the last kernel that read _dmsg[s]
+            self._wait_rows_free(stream)  # the last aggregation that read the rows
             d = self._dmsg[s]
             if d is None or d.numel() < msg.nbytes:
                 d = self._dmsg[s] = torch.empty(max(msg.nbytes, 1 << 20), dtype=torch.uint8, device=self.device)
@@ -870,22 +1021,7 @@ class DeviceInbox:
 
 
 _POOL = None
-_HASH_POOL = None
 _POOL_LOCK = threading.Lock()
-
-
-def _sha256(buf) -> bytes:
-    return hashlib.sha256(buf).digest()  # releases the GIL for large buffers
-
-
-def _hash_pool():
-    global _HASH_POOL
-    with _POOL_LOCK:
-        if _HASH_POOL is None:
-            from concurrent.futures import ThreadPoolExecutor
-            _HASH_POOL = ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1),
-                                            thread_name_prefix="p2p-sha256")
-        return _HASH_POOL
 
 
 def _copy_all(jobs) -> None:

@@ -94,8 +94,9 @@ def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor],
     ends with the identical global model -- byte-identical to one GPU.
     ``reduce(peers, w, rule, lr, trim_frac)`` defaults to the HIP kernels;
     tests substitute the CPU oracle to exercise the plan over gloo."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    gather = dist.is_initialized()  # a world of 1 still gathers (in place): the same call path
+    world = dist.get_world_size(group) if gather else 1
+    rank = dist.get_rank(group) if gather else 0
     n = w_full.numel()
     plan = ChunkPlan(n, world, max(1, min(chunk, -(-n // world))))
     reduce = reduce or _default_reduce
@@ -103,12 +104,12 @@ def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor],
     flat_peers = [p.reshape(-1) for p in peers_full]
     on_gpu = w.is_cuda
     comp = torch.cuda.current_stream(w.device) if on_gpu else None
-    comm = torch.cuda.Stream(w.device) if (on_gpu and overlap and world > 1) else None
+    comm = torch.cuda.Stream(w.device) if (on_gpu and overlap and gather) else None
     C, G = plan.chunk, world
     for s in range(plan.full_rounds):
         st = (s * G + rank) * C
         reduce([p[st:st + C] for p in flat_peers], w[st:st + C], rule, lr, trim_frac)
-        if world == 1:
+        if not gather:
             continue
         out = w[s * G * C:(s + 1) * G * C]
         mine = w[st:st + C]
@@ -124,7 +125,7 @@ def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor],
         st, ln = plan.tail_range(rank)
         if ln:
             reduce([p[st:st + ln] for p in flat_peers], w[st:st + ln], rule, lr, trim_frac)
-        if world > 1:
+        if gather:
             if comm is not None:
                 comp.wait_stream(comm)
             part = plan.tail_part

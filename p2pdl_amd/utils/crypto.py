@@ -3,16 +3,23 @@
 The reference signs / verifies with ``ec.ECDSA(hashes.SHA256())``
 (utils/crypto.py:54-57 and :92-96): OpenSSL hashes the full serialized update
 on every call -- 72 SHA-256 passes over 3 distinct messages per round in the
-default configuration.  Here the SHA-256 runs in the gfx950
-batch kernel (``p2p_sha256_batch``), once per DISTINCT message, and the EC
-step signs / verifies the 32-byte digest with ``Prehashed(SHA256())`` --
-byte-compatible with the reference's signatures because ECDSA signs the
-digest.  The EC arithmetic (out of scope) needs the ``cryptography`` package;
-it is imported lazily and is absent from this build image, so the EC half is
-"parity unpinned" here (DESIGN.md).
+default configuration.  Here every digest comes from
+``utils/digests.py``: each DISTINCT message is hashed once per process (at
+arrival by ``DeviceInbox.land(..., digest=True)``, or at its first sign /
+verify), later calls on the same object -- or on equal bytes -- reuse it, and
+the EC step signs / verifies the 32-byte digest with
+``Prehashed(SHA256())`` -- byte-compatible with the reference's signatures
+because ECDSA signs the digest.  Single messages hash on the host (SHA-NI);
+batches of many distinct messages go to the gfx950 batch kernel
+(``p2p_sha256_batch``; boundary in DESIGN.md §3 K3).  The EC arithmetic (out
+of scope) needs the ``cryptography`` package; it is imported lazily and is
+absent from this build image, so the EC half is "parity unpinned" here
+(DESIGN.md).
 
 Function names, arguments and the never-raise / return-False behaviour of
-``verify_signature`` mirror the reference (:64-101).
+``verify_signature`` mirror the reference (:64-101): a maintainer points
+``p2pdl/utils/crypto.py`` at this module and ``utils/broadcast.py`` (which
+imports sign_data / verify_signature from it, :4) is left untouched.
 """
 from __future__ import annotations
 
@@ -20,7 +27,7 @@ import logging
 import pickle
 from typing import Iterable, Sequence
 
-from .. import ops
+from . import digests
 
 
 class KeyServer:
@@ -60,23 +67,12 @@ def _ec():
     return hashes, ec, asym_utils
 
 
-def _as_bytes(data) -> bytes:
-    return data if isinstance(data, bytes) else pickle.dumps(data)  # reference :82-88
-
-
 def digest_updates(messages: Sequence[bytes]) -> list[bytes]:
-    """SHA-256 of every message in ONE GPU launch; a message that occurs
-    several times is hashed once (node/node.py:155,187-206 hash the same 3
-    updates 72 times per round)."""
-    uniq, index, slot = [], {}, []
-    for m in messages:
-        key = m if isinstance(m, bytes) else bytes(m)
-        if key not in index:
-            index[key] = len(uniq)
-            uniq.append(key)
-        slot.append(index[key])
-    d = ops.sha256_batch(uniq) if uniq else []
-    return [d[i] for i in slot]
+    """SHA-256 of every message; a message that occurs several times -- or
+    was hashed before -- is hashed once (node/node.py:155,187-206 hash the
+    same 3 updates 72 times per round).  Many distinct messages go to the
+    GPU batch kernel in one launch (``digests.digest_many``)."""
+    return digests.digest_many(messages)
 
 
 def generate_key_pair():
@@ -87,14 +83,16 @@ def generate_key_pair():
 
 
 def sign_data(private_key, data, digest: bytes | None = None):
-    """ECDSA(SHA-256(data)) like reference :50-59 -- the SHA-256 on the GPU,
-    the EC step on the 32-byte digest (Prehashed), which yields the same
-    signatures as ECDSA(SHA256()) over the data."""
+    """ECDSA(SHA-256(data)) like reference :50-59 -- the SHA-256 from the
+    digest cache (hashed once per distinct message), the EC step on the
+    32-byte digest (Prehashed), which yields the same signatures as
+    ECDSA(SHA256()) over the data.  ``data`` may also be a PinnedMessage
+    window (node/inbox.py) -- the serialized update where it arrived."""
     hashes, ec, asym_utils = _ec()
     if digest is None:
-        if not isinstance(data, (bytes, bytearray, memoryview)):
+        if not isinstance(data, (bytes, bytearray, memoryview)) and not digests._is_window(data):
             raise TypeError(f"data must be bytes-like, got {type(data).__name__}")  # as cryptography's sign
-        digest = digest_updates([data])[0]
+        digest = digests.digest_of(data)
     return private_key.sign(digest, ec.ECDSA(asym_utils.Prehashed(hashes.SHA256())))
 
 
@@ -112,13 +110,13 @@ def verify_signature(key_server, addr, port, data, signature, digest: bytes | No
         if data is None:
             logging.error(f"Cannot verify signature: data is None for {addr}:{port}")
             return False
-        if not isinstance(data, bytes):
+        if not isinstance(data, bytes) and not digests._is_window(data):
             try:
                 data = pickle.dumps(data)
             except Exception as e:
                 logging.error(f"Failed to serialize data for {addr}:{port}: {e}")
                 return False
-        digest = digest_updates([data])[0]
+        digest = digests.digest_of(data)
     try:
         public_key.verify(signature, digest, ec.ECDSA(asym_utils.Prehashed(hashes.SHA256())))
         return True
@@ -129,9 +127,10 @@ def verify_signature(key_server, addr, port, data, signature, digest: bytes | No
 
 def verify_signatures_batch(key_server, items: Iterable[tuple]) -> list[bool]:
     """verify_signature over many (addr, port, data, signature) items with
-    every distinct data blob hashed once, all in one GPU launch (the tester's
-    ready handler verifies the same bytes once per signature,
-    node/node.py:187-206).  Per-item results follow verify_signature."""
+    every distinct data blob hashed once (the tester's ready handler verifies
+    the same bytes once per signature, node/node.py:187-206); many distinct
+    blobs go to the GPU batch kernel in one launch.  Per-item results follow
+    verify_signature."""
     _ec()
     items = list(items)
     blobs, ok = [], []
@@ -140,17 +139,17 @@ def verify_signatures_batch(key_server, items: Iterable[tuple]) -> list[bool]:
             blobs.append(None)
             continue
         try:
-            blobs.append(data if isinstance(data, bytes) else pickle.dumps(data))
+            blobs.append(data if isinstance(data, bytes) or digests._is_window(data) else pickle.dumps(data))
         except Exception as e:
             logging.error(f"Failed to serialize data for {addr}:{port}: {e}")
             blobs.append(None)
     live = [b for b in blobs if b is not None]
-    digests = iter(digest_updates(live))
+    found = iter(digest_updates(live))
     for (addr, port, data, sig), b in zip(items, blobs):
         if b is None:
             if data is None:
                 logging.error(f"Cannot verify signature: data is None for {addr}:{port}")
             ok.append(False)
             continue
-        ok.append(verify_signature(key_server, addr, port, None, sig, digest=next(digests)))
+        ok.append(verify_signature(key_server, addr, port, None, sig, digest=next(found)))
     return ok

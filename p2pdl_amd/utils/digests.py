@@ -1,0 +1,267 @@
+"""SHA-256 of serialized updates, computed once per distinct message.
+
+The reference hashes the same serialized update inside every
+``ECDSA(SHA256())`` call (utils/crypto.py:54-57 sign, :92-96 verify): 72
+SHA-256 passes over 3 distinct messages per round in the default
+configuration (node/node.py:145,155,187-206).  This module
+keeps the digests this process has already computed, so ``sign_data`` /
+``verify_signature`` keep the reference's call signatures and still hash a
+message only the first time its bytes are seen:
+
+  * a hit by IDENTITY -- the same ``bytes`` object, or the same
+    ``PinnedMessage`` window (node/inbox.py) that ``DeviceInbox.land(...,
+    digest=True)`` hashed at arrival -- costs a dict lookup;
+  * a hit by CONTENT -- another object with equal bytes, e.g. the ready
+    message's copy of an update this node received earlier (node/node.py:175)
+    -- costs one memcmp (~10 GB/s on a host core, 4x cheaper than SHA-NI);
+  * a miss is hashed on the host (``hashlib``: one message is one serial
+    chain, ~2.4 GB/s with SHA-NI, against ~33 MB/s for one GPU lane chain --
+    DESIGN.md §3 K3), or, for a batch of many distinct messages, by the GPU
+    batch kernel (``digest_many``; the boundary is measured).
+
+Only immutable references are kept: ``bytes`` objects (held, bounded by
+count and bytes, least recently used evicted first) and ``PinnedMessage``
+windows (weakly: a window's buffer cannot return to the pool while it is
+alive, and the entry dies with it).  Equal digests are SHA-256 of equal
+bytes by construction, so a cache hit can never change a verification
+result.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import threading
+import weakref
+from collections import OrderedDict
+from concurrent.futures import Future
+
+import numpy as np
+
+_libc = ctypes.CDLL(None)
+_libc.memcmp.restype = ctypes.c_int
+_libc.memcmp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+
+_PROBE = 32  # bytes of head and tail in the content key
+
+
+def _buffer(data) -> memoryview:
+    """Byte view of bytes / bytearray / memoryview / PinnedMessage."""
+    view = getattr(data, "view", None)
+    if callable(view) and not isinstance(data, memoryview):
+        return view()
+    return memoryview(data).cast("B")
+
+
+def _address(mv: memoryview) -> int:
+    return np.frombuffer(mv, dtype=np.uint8).ctypes.data
+
+
+def _same_bytes(a: memoryview, b: memoryview) -> bool:
+    n = len(a)
+    if n != len(b):
+        return False
+    return n == 0 or _libc.memcmp(_address(a), _address(b), n) == 0
+
+
+def _is_window(data) -> bool:
+    return type(data).__name__ == "PinnedMessage" and hasattr(data, "root")
+
+
+class DigestCache:
+    """Digests by identity and by content (see the module docstring)."""
+
+    def __init__(self, max_entries: int = 256, max_bytes: int = 1 << 30):
+        self.max_entries, self.max_bytes = int(max_entries), int(max_bytes)
+        self._by_id: "OrderedDict[int, tuple]" = OrderedDict()  # id -> (ref, key)
+        self._by_key: dict = {}  # content key -> {id: (ref, digest or Future)}
+        self._held = 0  # bytes of strongly held `bytes` objects
+        self._lock = threading.Lock()
+        self.hits_identity = self.hits_content = self.misses = 0
+
+    @staticmethod
+    def _key(mv: memoryview):
+        n = len(mv)
+        return n, bytes(mv[:_PROBE]), bytes(mv[max(0, n - _PROBE):])
+
+    @staticmethod
+    def _alive(ref):
+        return ref() if isinstance(ref, weakref.ref) else ref
+
+    def clear(self) -> None:
+        with self._lock:
+            self._by_id.clear()
+            self._by_key.clear()
+            self._held = 0
+
+    def __len__(self) -> int:
+        return len(self._by_id)
+
+    def _drop_locked(self, oid: int) -> None:
+        ref, key = self._by_id.pop(oid)
+        bucket = self._by_key.get(key)
+        if bucket is not None:
+            bucket.pop(oid, None)
+            if not bucket:
+                del self._by_key[key]
+        if isinstance(ref, bytes):
+            self._held -= len(ref)
+
+    def put(self, data, digest) -> None:
+        """Remember ``digest`` (32 bytes, or a Future of them) for ``data``
+        when ``data`` is immutable for as long as the entry lives."""
+        if isinstance(data, bytes):
+            ref = data
+        elif _is_window(data):
+            oid0 = id(data)
+
+            def gone(_, oid=oid0, cache=self):
+                with cache._lock:
+                    ent = cache._by_id.get(oid)
+                    if ent is not None and isinstance(ent[0], weakref.ref) and ent[0]() is None:
+                        cache._drop_locked(oid)
+
+            ref = weakref.ref(data, gone)
+        else:
+            return  # mutable: looked up, never kept
+        key = self._key(_buffer(data))
+        oid = id(data)
+        with self._lock:
+            if oid in self._by_id:
+                self._drop_locked(oid)
+            self._by_id[oid] = (ref, key)
+            self._by_key.setdefault(key, {})[oid] = (ref, digest)
+            if isinstance(ref, bytes):
+                self._held += len(ref)
+            while self._by_id and (len(self._by_id) > self.max_entries or self._held > self.max_bytes):
+                self._drop_locked(next(iter(self._by_id)))
+
+    def get(self, data):
+        """The digest (or its Future) of ``data``'s bytes if known, else None."""
+        oid = id(data)
+        mv = _buffer(data)
+        key = self._key(mv)
+        with self._lock:
+            bucket = self._by_key.get(key)
+            if not bucket:
+                return None
+            ent = bucket.get(oid)
+            if ent is not None and self._alive(ent[0]) is data:
+                self._by_id.move_to_end(oid)
+                self.hits_identity += 1
+                return ent[1]
+            cands = [(self._alive(r), d) for r, d in bucket.values()]
+        for obj, d in cands:
+            if obj is not None and _same_bytes(mv, _buffer(obj)):
+                with self._lock:
+                    self.hits_content += 1
+                self.put(data, d)  # the next lookup of this object is by identity
+                return d
+        return None
+
+
+CACHE = DigestCache()
+_POOL = None
+_POOL_LOCK = threading.Lock()
+
+
+def hash_pool():
+    """Host hashing threads (hashlib releases the GIL on large buffers)."""
+    global _POOL
+    with _POOL_LOCK:
+        if _POOL is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            _POOL = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1), thread_name_prefix="p2p-sha256")
+        return _POOL
+
+
+def _result(d) -> bytes:
+    return d.result() if isinstance(d, Future) else d
+
+
+def sha256_host(data) -> bytes:
+    return hashlib.sha256(_buffer(data)).digest()
+
+
+def digest_of(data) -> bytes:
+    """SHA-256 of one message: from the cache, else hashed on the host once."""
+    d = CACHE.get(data)
+    if d is not None:
+        return _result(d)
+    with CACHE._lock:
+        CACHE.misses += 1
+    d = sha256_host(data)
+    CACHE.put(data, d)
+    return d
+
+
+def digest_async(data) -> Future:
+    """digest_of on a hashing thread (DeviceInbox.land(..., digest=True)):
+    the Future is registered at once, so a sign / verify of the same object
+    issued before the hash finishes waits for it instead of hashing again."""
+    d = CACHE.get(data)
+    if d is not None:
+        if isinstance(d, Future):
+            return d
+        f = Future()
+        f.set_result(d)
+        return f
+    with CACHE._lock:
+        CACHE.misses += 1
+    fut = hash_pool().submit(sha256_host, data)
+    CACHE.put(data, fut)
+    return fut
+
+
+# Below this many distinct uncached messages the host threads win; at and
+# above it the GPU batch kernel does (one lane chain per message, so many
+# short messages; measured boundary).
+GPU_BATCH_MIN = 2048
+
+
+def digest_many(messages) -> list:
+    """SHA-256 of every message, each distinct message hashed at most once:
+    cached ones from the cache, the rest on the host threads or -- for
+    GPU_BATCH_MIN or more of them -- in ONE launch of the GPU batch kernel
+    (``ops.sha256_batch``)."""
+    messages = list(messages)
+    out = [None] * len(messages)
+    todo = []  # (index, message) of cache misses
+    for i, m in enumerate(messages):
+        d = CACHE.get(m)
+        if d is None:
+            todo.append(i)
+        else:
+            out[i] = d
+    if todo:
+        uniq, slot, seen = [], {}, {}  # distinct misses: by identity, then by content
+        for i in todo:
+            m = messages[i]
+            j = seen.get(id(m))
+            if j is None:
+                mv = _buffer(m)
+                for j0 in seen.get(DigestCache._key(mv), ()):
+                    if _same_bytes(mv, _buffer(uniq[j0])):
+                        j = j0
+                        break
+                if j is None:
+                    j = len(uniq)
+                    uniq.append(m if isinstance(m, bytes) else bytes(mv))
+                    seen.setdefault(DigestCache._key(mv), []).append(j)
+                seen[id(m)] = j
+            slot[i] = j
+        with CACHE._lock:
+            CACHE.misses += len(uniq)
+        if len(uniq) >= GPU_BATCH_MIN:
+            from .. import ops
+
+            ds = ops.sha256_batch(uniq)
+        elif len(uniq) == 1:
+            ds = [sha256_host(uniq[0])]
+        else:
+            ds = list(hash_pool().map(sha256_host, uniq))
+        for i in todo:
+            out[i] = ds[slot[i]]
+            CACHE.put(messages[i], out[i])
+    return [_result(d) for d in out]

@@ -17,7 +17,8 @@ import types
 
 import pytest
 
-from p2pdl_amd.utils import crypto
+from p2pdl_amd import ops
+from p2pdl_amd.utils import crypto, digests
 
 
 class FakeAlg:
@@ -56,18 +57,27 @@ class FakePublicKey:
 
 @pytest.fixture
 def env(monkeypatch):
-    launches = []
+    launches, hashed = [], []
 
     def sha256_batch(msgs, device=None):  # hashlib in place of the GPU launch (CPU test)
         launches.append(list(msgs))
         return [hashlib.sha256(m).digest() for m in msgs]
 
+    real_host = digests.sha256_host
+
+    def sha256_host(data):
+        hashed.append(bytes(digests._buffer(data)))
+        return real_host(data)
+
     monkeypatch.setattr(crypto, "_ec", fake_ec)
-    monkeypatch.setattr(crypto.ops, "sha256_batch", sha256_batch)
+    monkeypatch.setattr(ops, "sha256_batch", sha256_batch)
+    monkeypatch.setattr(digests, "sha256_host", sha256_host)
+    digests.CACHE.clear()
     ks = crypto.KeyServer()
     pub = FakePublicKey()
     ks.register_key("127.0.0.1", 7001, pub)
-    return types.SimpleNamespace(ks=ks, pub=pub, priv=FakePrivateKey(), launches=launches)
+    yield types.SimpleNamespace(ks=ks, pub=pub, priv=FakePrivateKey(), launches=launches, hashed=hashed)
+    digests.CACHE.clear()
 
 
 def test_sign_then_verify_roundtrip(env):
@@ -102,17 +112,52 @@ def test_non_bytes_data_is_pickled_like_the_reference(env):
         crypto.sign_data(env.priv, obj)
 
 
-def test_72_hashes_become_3_in_one_launch(env):
+def test_72_hashes_become_3(env):
     """Default round: 3 distinct updates, 4 testers x 3 readies x
     4 signatures + echo verifies = 72 hash passes in the reference."""
     updates = [pickle.dumps({"trainer": t, "w": bytes(range(256)) * (t + 1)}) for t in range(3)]
     sigs = {u: crypto.sign_data(env.priv, u) for u in updates}
-    env.launches.clear()
     items = [("127.0.0.1", 7001, u, sigs[u]) for _ in range(24) for u in updates]
     assert len(items) == 72
     assert crypto.verify_signatures_batch(env.ks, items) == [True] * 72
-    assert len(env.launches) == 1 and sorted(env.launches[0]) == sorted(updates)
+    assert sorted(env.hashed) == sorted(updates) and env.launches == []  # 3 host hashes, no launch
     assert env.pub.calls == 72  # the EC check still runs per signature
+
+
+def test_reference_round_with_reference_call_signatures(env):
+    """The reference's own per-round calls, unchanged (node/node.py:145 ->
+    utils/broadcast.py:14, :155, :202), on the objects the reference holds:
+    each tester's copy of an update comes out of its own pickle.loads of the
+    envelope (:112), the ready message carries yet another copy (:175).
+    Each distinct update is hashed once; every other call is a cache hit by
+    identity or by content."""
+    updates = [pickle.dumps({"trainer": t, "w": bytes(range(256)) * (50 + t)}) for t in range(3)]
+    testers = 4
+    copies = [[pickle.loads(pickle.dumps({"model": u}))["model"] for u in updates] for _ in range(testers)]
+    sig = {}
+    for i in range(testers):  # 12 echo signs over each tester's own copy
+        for t in range(3):
+            sig[i, t] = crypto.sign_data(env.priv, copies[i][t])
+    for t in range(3):  # 12 echo verifies over the trainer's own local_update (:155)
+        for i in range(testers):
+            assert crypto.verify_signature(env.ks, "127.0.0.1", 7001, updates[t], sig[i, t])
+    for i in range(testers):  # 48 ready verifies: per ready message, its own copy (:175, :202)
+        for t in range(3):
+            ready_copy = pickle.loads(pickle.dumps({"local_update": updates[t]}))["local_update"]
+            for j in range(testers):
+                assert crypto.verify_signature(env.ks, "127.0.0.1", 7001, ready_copy, sig[j, t])
+    assert env.pub.calls == 60 and len(env.hashed) == 3
+    assert digests.CACHE.hits_content >= 3 and digests.CACHE.hits_identity >= 40
+
+
+def test_many_distinct_messages_take_the_gpu_batch(env, monkeypatch):
+    monkeypatch.setattr(digests, "GPU_BATCH_MIN", 3)
+    msgs = [b"b", b"a", b"b", bytearray(b"a"), b"", b"c"]
+    got = crypto.digest_updates(msgs)
+    assert got == [hashlib.sha256(bytes(m)).digest() for m in msgs]
+    assert env.launches == [[b"b", b"a", b"", b"c"]] and env.hashed == []
+    env.launches.clear()
+    assert crypto.digest_updates(msgs) == got and env.launches == []  # all cached now
 
 
 def test_batch_mixed_results(env):
@@ -122,16 +167,39 @@ def test_batch_mixed_results(env):
              ("10.0.0.9", 9, good, b"x"),
              ("127.0.0.1", 7001, None, b"x"),
              ("127.0.0.1", 7001, lambda: 0, b"x")]
-    env.launches.clear()
+    env.hashed.clear()
     assert crypto.verify_signatures_batch(env.ks, items) == [True, False, False, False, False]
-    assert env.launches == [[good]]
+    assert env.hashed == []  # signed above: cached
 
 
 def test_digest_updates_dedupes_and_keeps_order(env):
     msgs = [b"b", b"a", b"b", bytearray(b"a"), b""]
     got = crypto.digest_updates(msgs)
     assert got == [hashlib.sha256(bytes(m)).digest() for m in msgs]
-    assert env.launches == [[b"b", b"a", b""]]
+    assert sorted(env.hashed) == [b"", b"a", b"b"] and env.launches == []
+
+
+def test_cache_content_hit_needs_equal_bytes(env):
+    """Same length, head and tail but one byte different in the middle: a
+    miss (the memcmp decides), with the right digest."""
+    a = bytes(100) + b"x" + bytes(100)
+    b = bytes(100) + b"y" + bytes(100)
+    assert digests.digest_of(a) == hashlib.sha256(a).digest()
+    assert digests.digest_of(b) == hashlib.sha256(b).digest()
+    assert digests.digest_of(bytearray(b)) == hashlib.sha256(b).digest()
+    assert len(env.hashed) == 2
+
+
+def test_cache_is_bounded(env):
+    cache = digests.DigestCache(max_entries=4, max_bytes=1000)
+    msgs = [bytes([i]) * 300 for i in range(6)]
+    for m in msgs:
+        cache.put(m, hashlib.sha256(m).digest())
+    assert len(cache) <= 3 and cache._held <= 1000
+    assert cache.get(msgs[-1]) == hashlib.sha256(msgs[-1]).digest()
+    assert cache.get(msgs[0]) is None  # least recently used went first
+    cache.put(bytearray(b"mutable"), bytes(32))  # never kept
+    assert cache.get(b"mutable") is None
 
 
 def test_missing_cryptography_raises_importerror(monkeypatch):
@@ -169,11 +237,15 @@ def test_key_server_semantics(caplog):
 
 @pytest.mark.gpu
 def test_gpu_digests_match_hashlib_with_dedupe(cuda, monkeypatch):
-    """The real HIP batch kernel behind digest_updates: 72 items, 3 distinct."""
+    """The real HIP batch kernel behind digest_updates (the GPU boundary set
+    low): 72 items, 3 distinct, one launch over the 3."""
     calls = []
-    real = crypto.ops.sha256_batch
-    monkeypatch.setattr(crypto.ops, "sha256_batch", lambda m, device=None: calls.append(len(m)) or real(m, device))
+    real = ops.sha256_batch
+    monkeypatch.setattr(ops, "sha256_batch", lambda m, device=None: calls.append(len(m)) or real(m, device))
+    monkeypatch.setattr(digests, "GPU_BATCH_MIN", 2)
+    digests.CACHE.clear()
     updates = [pickle.dumps({"t": t, "w": bytes(range(256)) * (1000 + 37 * t)}) for t in range(3)]
     msgs = [u for _ in range(24) for u in updates]
     assert crypto.digest_updates(msgs) == [hashlib.sha256(m).digest() for m in msgs]
     assert calls == [3]
+    digests.CACHE.clear()

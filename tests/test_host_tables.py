@@ -39,3 +39,19 @@ def test_size_mismatch_rejected(numels, shape):
     received = [{"model": {"a": torch.zeros(2), "b": torch.zeros(2)}}]
     with pytest.raises(ValueError):
         _host_tables.gather_peer_table(received, ["a", "b"], numels, 0, np.zeros(shape, dtype=np.uint64))
+
+
+def test_sparse_tensor_defers_to_python_path():
+    """the layout is checked before is_contiguous (which throws
+    c10::Error on a sparse tensor and used to end in std::terminate)."""
+    sp = torch.sparse_coo_tensor(torch.tensor([[0, 1]]), torch.tensor([1.0, 2.0]), (2,))
+    assert _host_tables.gather_peer_table([{"model": {"a": sp}}], ["a"], [2], -1, _table(1, 1)) == 1
+
+
+@pytest.mark.gpu
+def test_sparse_cuda_tensor_defers_to_python_path(cuda):
+    sp = torch.sparse_coo_tensor(torch.tensor([[0, 1]]), torch.tensor([1.0, 2.0]), (2,)).to(cuda)
+    dense = torch.zeros(2, device=cuda)
+    got = _host_tables.gather_peer_table([{"model": {"a": dense}}, {"model": {"a": sp}}], ["a"], [2],
+                                         cuda.index, _table(1, 2))
+    assert got == 1

@@ -1,0 +1,288 @@
+"""Receive-buffer ownership, envelopes and slab-row reuse (node/inbox.py).
+
+ADVICE r03: a pinned receive buffer must not return to the pool while the
+listener can still read it (the echo reads the serialized update after
+landing, node/node.py:145 -> utils/broadcast.py:14,23); only the 'model' of a
+'model_update' may be a window of it, every other envelope decodes as the
+reference decodes it (pickle.loads at node/node.py:112); a peer's length
+field cannot pin host memory.  VERDICT r03 weak #7: landing round r+1 into
+a row waits for round r's kernel that reads it.
+
+CPU tests run the host logic over pageable stand-ins for the pinned buffers
+(the ``_pinned_bytes`` seam); GPU tests run the real inbox.
+"""
+import collections
+import hashlib
+import pickle
+import socket
+import threading
+import types
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import assert_bits_equal
+from p2pdl_amd.node import inbox as inbox_mod
+from p2pdl_amd.node.inbox import DeviceInbox, PinnedMessage, _PinnedBuffer, recv_body
+from p2pdl_amd.utils import digests
+
+
+class FakePool:
+    def __init__(self):
+        self.back = []
+
+    def _release(self, root):
+        self.back.append(root)
+
+
+@pytest.fixture
+def pageable(monkeypatch):
+    monkeypatch.setattr(inbox_mod, "_pinned_bytes", lambda n: torch.empty(n, dtype=torch.uint8))
+    return FakePool()
+
+
+def message(pool, data: bytes) -> PinnedMessage:
+    root = _PinnedBuffer(len(data), pool)
+    m = PinnedMessage(root, 0, len(data))
+    m.buf[:len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    return m
+
+
+def open_envelope(msg):
+    return DeviceInbox.open_envelope(None, msg)  # uses no inbox state
+
+
+def test_model_update_envelope_model_is_a_window_that_holds_the_buffer(pageable):
+    ser = pickle.dumps({"w": torch.arange(10, dtype=torch.float32)})
+    env = pickle.dumps({"type": "model_update", "model": ser, "addr": "127.0.0.1", "port": 5001})
+    msg = message(pageable, env)
+    root = msg.root
+    cmd = open_envelope(msg)
+    assert isinstance(cmd["model"], PinnedMessage) and bytes(cmd["model"]) == ser
+    assert cmd["type"] == "model_update" and cmd["addr"] == "127.0.0.1" and cmd["port"] == 5001
+    assert pageable.back == []  # the window holds the buffer
+    # the echo pickles the serialized update (utils/broadcast.py:18-24): as bytes
+    echo = pickle.loads(pickle.dumps({"type": "echo", "serialized_state": cmd["model"]}))
+    assert type(echo["serialized_state"]) is bytes and echo["serialized_state"] == ser
+    cmd["model"].release()
+    assert pageable.back == [root]
+    with pytest.raises(ValueError):
+        cmd["model"].view()  # released: the buffer may hold another message
+
+
+def test_window_dropped_returns_the_buffer(pageable):
+    ser = pickle.dumps({"w": torch.zeros(3)})
+    cmd = open_envelope(message(pageable, pickle.dumps({"type": "model_update", "model": ser,
+                                                         "addr": "a", "port": 1})))
+    assert pageable.back == []
+    del cmd  # the listener's frame ends (node/node.py:246-249)
+    assert len(pageable.back) == 1
+
+
+@pytest.mark.parametrize("kind", ["echo", "ready", "sup", "connect", "global_model_update", "tensor_model"])
+def test_other_envelopes_decode_like_the_reference(pageable, kind):
+    """Every value is a plain object (bytes, not windows) and the buffer goes
+    back to the pool at once."""
+    upd = pickle.dumps({"w": torch.arange(6, dtype=torch.float32)})
+    sig = [b"\x30\x45" + bytes(range(60)), b"\x30\x44" + bytes(range(59))]
+    envs = {
+        "echo": {"type": "echo", "signature": sig[0], "addr": "a", "port": 1, "serialized_state": upd},
+        "ready": {"type": "ready", "signature_list": sig, "addr": "a", "port": 1,
+                  "sender_list": [{"addr": "b", "port": 2}, {"addr": "c", "port": 3}], "local_update": upd},
+        "sup": {"type": "sup", "signature_list": sig, "addr": "a", "port": 1, "model_update": None},
+        "connect": {"type": "connect", "addr": "a", "port": 1},
+        # aggregation.py:70 pickles the global state_dict of tensors (torch globals)
+        "global_model_update": {"type": "global_model_update", "addr": "a", "port": 1,
+                                "model": collections.OrderedDict(w=torch.arange(4.0), b=torch.ones(2))},
+        # a model_update whose 'model' is not serialized bytes
+        "tensor_model": {"type": "model_update", "addr": "a", "port": 1, "model": {"w": torch.ones(2)}},
+    }
+    data = pickle.dumps(envs[kind])
+    got = open_envelope(message(pageable, data))
+    want = pickle.loads(data)
+    assert list(got) == list(want)
+    for k in want:
+        if isinstance(want[k], dict):
+            assert list(got[k]) == list(want[k])
+            for a in want[k]:
+                assert torch.equal(got[k][a], want[k][a]) if torch.is_tensor(want[k][a]) else got[k][a] == want[k][a]
+        else:
+            assert got[k] == want[k] and type(got[k]) is type(want[k]), k
+    assert len(pageable.back) == 1
+
+
+def test_pool_is_bounded_by_bytes():
+    pool = types.SimpleNamespace(_lock=threading.Lock(), _pinned_free=[], pool_bytes=1000)
+    roots = [types.SimpleNamespace(capacity=c) for c in (400, 400, 400, 100)]
+    for r in roots:
+        DeviceInbox._release(pool, r)
+    assert pool._pinned_free == [roots[0], roots[1], roots[3]]  # the third 400 would exceed 1000
+    DeviceInbox._release(pool, roots[0])  # idempotent
+    assert len(pool._pinned_free) == 3
+
+
+def test_recv_body_grows_as_bytes_arrive(monkeypatch):
+    monkeypatch.setattr(inbox_mod, "_RECV_STEP", 1000)
+    data = bytes(range(256)) * 30  # 7680 B: 1000 -> 2000 -> 4000 -> 7680
+    a, b = socket.socketpair()
+    th = threading.Thread(target=lambda: (a.sendall(data), a.close()))
+    th.start()
+    assert bytes(recv_body(b, len(data))) == data
+    th.join(10)
+    b.close()
+    c, d = socket.socketpair()
+    c.sendall(b"x" * 1500)
+    c.close()
+    assert recv_body(d, 1 << 40) is None  # a bogus length: early close, ~2 KB ever allocated
+    d.close()
+
+
+def test_signing_a_landed_window_reuses_the_arrival_digest(pageable, monkeypatch):
+    """land(window, digest=True) registers the Future under the window itself:
+    the echo's sign_data(private_key, window) is an identity hit."""
+    digests.CACHE.clear()
+    hashed = []
+    real = digests.sha256_host
+    monkeypatch.setattr(digests, "sha256_host", lambda d: hashed.append(1) or real(d))
+    ser = pickle.dumps({"w": torch.arange(1000, dtype=torch.float32)})
+    cmd = open_envelope(message(pageable, pickle.dumps({"type": "model_update", "model": ser,
+                                                         "addr": "a", "port": 1})))
+    fut = digests.digest_async(cmd["model"])  # what land(..., digest=True) starts
+    assert digests.digest_of(cmd["model"]) == fut.result() == hashlib.sha256(ser).digest()
+    assert digests.digest_of(bytes(ser)) == fut.result()  # equal bytes elsewhere: content hit
+    assert len(hashed) == 1
+    w = cmd["model"]
+    del cmd
+    w.release()
+    del w
+    assert len(digests.CACHE) == 1  # the window's entry died with it; the bytes copy's stays
+    digests.CACHE.clear()
+
+
+# ----------------------------------------------------------------- GPU
+MLP_SHAPES = [("fc1.weight", (512, 784)), ("fc1.bias", (512,)), ("fc2.weight", (256, 512)),
+              ("fc2.bias", (256,)), ("fc3.weight", (10, 256)), ("fc3.bias", (10,))]  # models/model.py:6-8
+
+
+def mlp_update(seed):
+    return {k: torch.from_numpy(oracle.synth(int(np.prod(s)), seed, i, 1e-2).reshape(s))
+            for i, (k, s) in enumerate(MLP_SHAPES)}
+
+
+def _send(conn, data):
+    th = threading.Thread(target=lambda: (conn.sendall(len(data).to_bytes(4, "big") + data), conn.close()))
+    th.start()
+    return th
+
+
+@pytest.mark.gpu
+def test_message_over_the_cap_arrives_pageable(cuda):
+    template = {k: torch.zeros(s, device=cuda) for k, s in MLP_SHAPES}
+    inbox = DeviceInbox(template, k_max=2, device=cuda, max_message_bytes=1 << 20)
+    data = pickle.dumps(mlp_update(3))  # 2.1 MB > 1 MiB cap
+    a, b = socket.socketpair()
+    th = _send(a, data)
+    got = inbox.recv(b)
+    th.join(10)
+    b.close()
+    assert type(got) is bytearray and bytes(got) == data and inbox._pinned_free == []
+    landed = inbox.land(got)
+    torch.cuda.synchronize()
+    ref = pickle.loads(data)
+    for k in ref:
+        assert_bits_equal(landed[k].cpu().numpy(), ref[k].numpy(), what=k)
+
+
+@pytest.mark.gpu
+def test_echo_bytes_stay_valid_while_another_listener_receives(cuda):
+    """listener A lands its update and reads the serialized bytes
+    for its echo AFTER landing while listener B receives the next message:
+    B gets another buffer, A's bytes are intact."""
+    template = {k: torch.zeros(s, device=cuda) for k, s in MLP_SHAPES}
+    inbox = DeviceInbox(template, k_max=2, device=cuda)
+    sers = [pickle.dumps(mlp_update(20 + j)) for j in range(2)]
+    envs = [pickle.dumps({"type": "model_update", "model": s, "addr": "a", "port": j}) for j, s in enumerate(sers)]
+    a, b = socket.socketpair()
+    th = _send(a, envs[0])
+    cmd_a = inbox.open_envelope(inbox.recv(b))
+    th.join(10)
+    inbox.land(cmd_a["model"], digest=True)
+    c, d = socket.socketpair()
+    th = _send(c, envs[1])
+    msg_b = inbox.recv(d)  # B's recv after A's land returned
+    th.join(10)
+    assert msg_b.root is not cmd_a["model"].root
+    assert bytes(cmd_a["model"].view()) == sers[0]  # A's echo bytes (utils/broadcast.py:14,23)
+    cmd_b = inbox.open_envelope(msg_b)
+    assert bytes(cmd_b["model"]) == sers[1]
+    for x in (b, d):
+        x.close()
+
+
+@pytest.mark.gpu
+def test_landing_next_round_waits_for_the_kernel_reading_the_rows(cuda, monkeypatch):
+    """round r's aggregation is queued behind a long
+    spin on the compute stream; round r+1 lands into the same rows from
+    another thread on a side stream.  The landing waits for the kernel, so
+    the model gets round r's mean -- no reliance on the broadcast's
+    synchronize (stubbed out here)."""
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    if not hasattr(torch.cuda, "_sleep"):
+        pytest.skip("torch.cuda._sleep unavailable")
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
+    n, k = 1 << 20, 3
+    template = {"w": torch.zeros(n, device=cuda)}
+    inbox = DeviceInbox(template, k_max=k, device=cuda)
+    w0 = oracle.synth(n, 9, 0xFFFFF, 5e-2)
+    model = torch.nn.Module()
+    model.register_parameter("w", torch.nn.Parameter(torch.from_numpy(w0.copy()).to(cuda), requires_grad=False))
+    rounds = [[oracle.synth(n, 9, 10 * r + j, 1e-2) for j in range(k)] for r in range(2)]
+    for pinned in (False, True):
+        with torch.no_grad():
+            model.w.copy_(torch.from_numpy(w0))
+        inbox.reset()
+        sers = [[pickle.dumps({"w": torch.from_numpy(u)}) for u in rnd] for rnd in rounds]
+        landed = [inbox.land(s) for s in sers[0]]
+        node = types.SimpleNamespace(model=model, trainers_list=[0] * k, addr="a", port=1, neighbors=[],
+                                     received_models=[{"model": u, "sender": j} for j, u in enumerate(landed)])
+        torch.cuda.synchronize()
+        torch.cuda._sleep(400_000_000)  # ~0.2 s of spinning ahead of the aggregation kernel
+        agg.aggregate_models(node)
+        side = torch.cuda.Stream(cuda)
+
+        def next_round():
+            with torch.cuda.stream(side):
+                inbox.reset()
+                for s in sers[1]:
+                    if pinned:
+                        m = inbox.message_buffer(len(s))
+                        m.buf[:len(s)].copy_(torch.frombuffer(bytearray(s), dtype=torch.uint8))
+                        inbox.land(m)
+                    else:
+                        inbox.land(s)
+
+        th = threading.Thread(target=next_round)
+        th.start()
+        th.join(60)
+        torch.cuda.synchronize()
+        want, _ = oracle.fedavg(rounds[0], w0)
+        assert_bits_equal(model.w.detach().cpu().numpy(), want, what=f"pinned={pinned}")
+
+
+@pytest.mark.gpu
+def test_payload_outside_the_message_is_refused(cuda):
+    """a segment whose source lies outside the message
+    raises instead of landing the kernel's zero fill."""
+    template = {"w": torch.zeros(16, device=cuda)}
+    inbox = DeviceInbox(template, k_max=1, device=cuda)
+    data = pickle.dumps({"w": torch.arange(16, dtype=torch.float32)})
+    other = pickle.dumps({"w": torch.arange(16, dtype=torch.float32) + 1})
+    m = inbox.message_buffer(len(data))
+    m.buf[:len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    raw = inbox_mod.ZeroCopyParser(other).parse()  # payload addresses of another buffer
+    with pytest.raises(pickle.UnpicklingError):
+        with inbox._lock:
+            inbox._land_pinned_locked(m, raw, 0)
