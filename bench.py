@@ -84,9 +84,13 @@ WORKLOADS = {
     # land 16 serialized ResNet-18-sized updates (11.7M
     # params each) in the device slab vs the reference's pickle.loads
     "inbox": ("inbox", 16, 11_689_512, 0x5EED0007),
+    # the reference's per-round digest work: 72 sign/verify hashes over 3 MLP
+    # updates, through crypto.sign_data / verify_signature
+    "digest-flow": ("digest-flow", 3, 535_818, 0),
 }
-SUB_N1 = ["cfg1", "cfg2-dropin", "cfg4-median", "cfg4-trimmed", "median256", "trimmed256", "cfg5", "delta", "inbox"]
-SUB_STEPS = {"cfg5": 2, "delta": 10, "inbox": 3}  # timed steps of the one-GPU sub-records
+SUB_N1 = ["cfg1", "cfg2-dropin", "cfg4-median", "cfg4-trimmed", "median256", "trimmed256", "cfg5", "delta", "inbox",
+          "digest-flow"]
+SUB_STEPS = {"cfg5": 2, "delta": 10, "inbox": 3, "digest-flow": 5}  # timed steps of the one-GPU sub-records
 MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
 
@@ -472,6 +476,18 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
             e1.record(comp)
             ev.append((e0, e1))
 
+    def timed_calls():
+        # host wall time per call, the same way for both paths: no events
+        # inside the timed loop (the kernel is timed in a separate pass)
+        for _ in range(max(warmup, 2)):
+            call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
     try:
         call()
         torch.cuda.synchronize()
@@ -486,25 +502,15 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
             log(f"{name}: drop-in spot check vs oracle ({m} coords): {'bit-exact' if ok else 'MISMATCH'}")
             if not ok:
                 raise SystemExit(f"bench: {name} drop-in differs from the oracle")
-        for _ in range(max(warmup, 2)):
-            call()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
+        step_s = timed_calls()
+        for _ in range(steps):  # the kernel (+ table) time, HIP events around each call
             call(record=True)
         torch.cuda.synchronize()
-        step_s = (time.perf_counter() - t0) / steps
         ev_fast = list(ev)
         # the general path (plain dicts of tensors, e.g. from pickle.loads):
-        # per-tensor checks on the host for all L x K update tensors
+        # the peer table gathered in C from the L x K update tensors
         updates = plain
-        call()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            call()
-        torch.cuda.synchronize()
-        general_s = (time.perf_counter() - t0) / steps
+        general_s = timed_calls()
         ev.clear()
     finally:
         agg.broadcast_global_model_update = saved
@@ -542,9 +548,11 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
         "config": {"workload": f"{name}: drop-in aggregate_models, {len(sizes)}-tensor state_dict "
                                f"({n:,} params) x {K} updates landed in a DeviceInbox slab, one "
                                f"segment-table launch per call",
-                   "peers": K, "coords_per_gpu": n, "tensors": len(sizes), "parallelism": "single GPU"},
+                   "peers": K, "coords_per_gpu": n, "tensors": len(sizes), "parallelism": "single GPU",
+                   "us_per_call": round(step_s * 1e6, 1), "us_per_call_general_path": round(general_s * 1e6, 1)},
         "roofline": roofline(4 * n * (K + 2), call_ms, traffic_for(name, n, K),
-                             timing="HIP events around aggregate_models (table H2D + segment kernel)",
+                             timing="HIP events around aggregate_models (table H2D + segment kernel), in a "
+                                    "pass after the timed loops (value / us_per_call: host wall time, no events)",
                              flat_kernel_ms=round(flat_ms, 4),
                              vs_flat_kernel=round(flat_ms / call_ms, 4)),
         "cpu_baseline": cpu,
@@ -850,6 +858,121 @@ def run_inbox_workload(args, K, n, seed, dev):
                                                f"(node/node.py:135), same process"}}
 
 
+def run_digest_flow(args, steps):
+    """The reference's per-round digest work, through the
+    product's sign_data / verify_signature with the reference's call
+    signatures: 3 trainers' serialized MNIST-MLP updates (node/node.py:285),
+    4 testers -- 12 echo signs over each tester's own copy (node/node.py:145
+    -> utils/broadcast.py:14), 12 echo verifies over the trainer's
+    local_update (:155), 48 ready verifies over each ready message's copy
+    (:175,:202): 72 SHA-256 passes in the reference (ECDSA(SHA256()) hashes
+    its input on every call).  The objects are the ones the reference
+    holds: each copy comes out of its own pickle round trip.  The EC step is
+    stubbed on both sides (`cryptography` is absent from the image; it costs
+    the same per signature either way).  Each step is a new round: the
+    digest cache starts empty."""
+    import hashlib
+    import pickle
+
+    import numpy as np
+
+    from p2pdl_amd.utils import crypto, digests
+
+    class Key:  # ECDSA stand-in over the 32-byte digest
+        def sign(self, digest, alg):
+            return b"sig:" + digest
+
+        def verify(self, signature, digest, alg):
+            if signature != b"sig:" + digest:
+                raise ValueError("bad signature")
+
+    fake = (types.SimpleNamespace(SHA256=lambda: None), types.SimpleNamespace(ECDSA=lambda a: a),
+            types.SimpleNamespace(Prehashed=lambda h: h))
+    saved_ec = crypto._ec
+    crypto._ec = lambda: fake
+    ks, key = crypto.KeyServer(), Key()
+    ks.register_key("127.0.0.1", 1, key)
+    testers = 4
+    try:
+        def make_round(seed):
+            ups = []
+            for t in range(3):
+                rng = np.random.default_rng(seed * 10 + t)
+                ups.append(pickle.dumps({nm: torch.from_numpy(rng.standard_normal(s, dtype=np.float32) * 1e-2)
+                                         for nm, s in MLP_SHAPES}))
+            copies = [[pickle.loads(pickle.dumps({"model": u}))["model"] for u in ups] for _ in range(testers)]
+            ready = [[pickle.loads(pickle.dumps({"local_update": u}))["local_update"] for u in ups]
+                     for _ in range(testers)]
+            return ups, copies, ready
+
+        def product(ups, copies, ready):
+            sig = {}
+            for i in range(testers):
+                for t in range(3):
+                    sig[i, t] = crypto.sign_data(key, copies[i][t])
+            ok = 0
+            for t in range(3):
+                for i in range(testers):
+                    ok += crypto.verify_signature(ks, "127.0.0.1", 1, ups[t], sig[i, t])
+            for i in range(testers):
+                for t in range(3):
+                    for j in range(testers):
+                        ok += crypto.verify_signature(ks, "127.0.0.1", 1, ready[i][t], sig[j, t])
+            return sig, ok
+
+        def reference(ups, copies, ready):
+            out = []
+            for i in range(testers):
+                for t in range(3):
+                    out.append(hashlib.sha256(copies[i][t]).digest())
+            for t in range(3):
+                for i in range(testers):
+                    out.append(hashlib.sha256(ups[t]).digest())
+            for i in range(testers):
+                for t in range(3):
+                    for j in range(testers):
+                        out.append(hashlib.sha256(ready[i][t]).digest())
+            return out
+
+        t_prod, t_ref, misses = [], [], []
+        for step in range(steps + 1):
+            rnd = make_round(step)
+            digests.CACHE.clear()
+            m0 = digests.CACHE.misses
+            t0 = time.perf_counter()
+            sig, ok = product(*rnd)
+            t1 = time.perf_counter()
+            ref = reference(*rnd)
+            t2 = time.perf_counter()
+            if ok != 60 or any(sig[i, t] != b"sig:" + hashlib.sha256(rnd[0][t]).digest()
+                               for i in range(testers) for t in range(3)):
+                raise SystemExit("bench: digest_flow signatures differ from hashlib")
+            if step:  # step 0 warms up
+                t_prod.append(t1 - t0)
+                t_ref.append(t2 - t1)
+                misses.append(digests.CACHE.misses - m0)
+        msg = len(rnd[0][0])
+    finally:
+        crypto._ec = saved_ec
+        digests.CACHE.clear()
+    tp, tr = min(t_prod), min(t_ref)
+    log(f"digest_flow: product {tp*1e3:.3f} ms ({misses[-1]} hashes) vs reference {tr*1e3:.3f} ms (72 hashes)")
+    hashed = 72 * msg
+    return {
+        "workload": "digest_flow", "value": round(hashed / tp / 1e9, 3), "unit": "GB/s", "steps": steps,
+        "ms_per_step": round(tp * 1e3, 4), "scaling": "weak", "dtype": "u32 (SHA-256)",
+        "data": "synthetic MNIST-MLP updates (models/model.py:6-8) pickled like node/node.py:285",
+        "config": {"workload": f"digest_flow: one round's 72 sign/verify digests over 3 updates of {msg:,} B, "
+                               f"4 testers (SURVEY.md §3D), reference call signatures, best of {steps} rounds",
+                   "reference_ms": round(tr * 1e3, 4), "speedup_vs_reference": round(tr / tp, 2),
+                   "hashes_product": misses[-1], "hashes_reference": 72, "message_bytes": msg,
+                   "parallelism": "host (one process)"},
+        "roofline": None,
+        "cpu_baseline": {"value": round(hashed / tr / 1e9, 3), "unit": "GB/s", "kind": "reference", "cores": 1,
+                         "sample": "the reference's 72 hashlib.sha256 passes (ECDSA(SHA256()) at "
+                                   "utils/crypto.py:56,95) over the same objects, same process"}}
+
+
 def replica_workload(args, name, dev):
     """cfg5 / sha256 / delta / inbox (one GPU each): the workload's record."""
     rule, K, n, seed = WORKLOADS[name]
@@ -857,6 +980,8 @@ def replica_workload(args, name, dev):
         K, n = args.peers or K, args.coords or n
     if rule in ("fused", "sha256"):
         return run_digest_workload(args, rule, K, n, seed, dev)
+    if rule == "digest-flow":
+        return run_digest_flow(args, args.steps)
     if rule == "delta":
         return run_delta_workload(args, n, seed, dev)
     return run_inbox_workload(args, K, n, seed, dev)
@@ -883,7 +1008,8 @@ def compact_sub(rec: dict) -> dict:
         if alg and tr:
             out["traffic_x"] = round(tr / alg, 5)
     cfg = rec.get("config") or {}
-    for k in ("reference_ms", "staging_ms", "pinned_digest_overlapped_ms", "with_digest"):
+    for k in ("reference_ms", "staging_ms", "pinned_digest_overlapped_ms", "with_digest", "hashes_product",
+              "speedup_vs_reference"):
         if k in cfg:
             v = cfg[k]
             out[k] = {a: b for a, b in v.items() if a != "what"} if isinstance(v, dict) else v
@@ -968,10 +1094,11 @@ def main():
     K = args.peers or K
     n = args.coords or n
     one_gpu = {"fused": "cfg5/sha256 run as replicas only", "sha256": "cfg5/sha256 run as replicas only",
+               "digest-flow": "digest-flow runs in one process",
                "delta": "delta runs as replicas only", "inbox": "inbox runs on one GPU", "dropin": "drop-in runs on one GPU"}
     if rule in one_gpu and world > 1:
         raise SystemExit(one_gpu[rule] + " (one process per GPU)")
-    if rule in ("fused", "sha256", "delta", "inbox"):
+    if rule in ("fused", "sha256", "delta", "inbox", "digest-flow"):
         rec = replica_workload(args, args.workload, dev)
         print(json.dumps({"metric": METRIC, "value": rec["value"], "unit": rec["unit"], "n_gpus": 1,
                           "steps": rec["steps"], "warmup": args.warmup, "ms_per_step": rec["ms_per_step"],
@@ -1006,7 +1133,7 @@ def main():
                     r, k2, n2, s2 = WORKLOADS[name]
                     if r == "dropin":
                         rec = measure_dropin(c, args, name, k2, s2, 30, 2, args.sub_cpu_seconds)
-                    elif r in ("fused", "delta", "inbox"):
+                    elif r in ("fused", "delta", "inbox", "digest-flow"):
                         sargs = argparse.Namespace(**dict(vars(args), workload=name, steps=SUB_STEPS[name],
                                                           warmup=1, cpu_seconds=args.sub_cpu_seconds))
                         rec = replica_workload(sargs, name, dev)

@@ -31,7 +31,9 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..node.inbox import LandedUpdate
 from ..utils.waiting import wait_for_models
+from .model_state import model_state
 
 try:  # host-side C gather of the peer table (p2pdl_amd/csrc/host_tables.cpp)
     from .. import _host_tables
@@ -59,9 +61,10 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
         logging.error(f"[{self.addr}:{self.port}] No updates received to aggregate!")
         return
 
-    state = self.model.state_dict()
-    keys = list(state.keys())
-    if _slab_fast_path(state, keys, received, rule or AGGREGATION_RULE, lr, trim_frac):
+    # keys and tensors of self.model.state_dict() (:15,:27,:37), from a cache
+    # re-validated against the model on every call (model_state.py)
+    keys, ws, st = model_state(self.model)
+    if _slab_fast_path(st, keys, ws, received, rule or AGGREGATION_RULE, lr, trim_frac):
         logging.info(f"[{self.addr}:{self.port}] Model aggregation completed, applied local updates.")
         self.received_models.clear()
         broadcast_global_model_update(self)
@@ -69,23 +72,25 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
     # The (L, K) peer table gathered in C when every update tensor is a plain
     # fp32 tensor on the model's device (KeyError on a missing key, like :28);
     # otherwise the per-tensor path below, with the exact diagnosis.
-    table = _gather_table(received, keys, state)
+    table = _gather_table(received, keys, ws)
     if table is None:
         updates = []
         for received_model in received:  # KeyError on a missing key, like :28
             local_update = received_model["model"]
             updates.append([local_update[key] for key in keys])
 
-    for key in keys:  # the reference raises at the division for integer tensors (:32)
-        t = state[key]
-        if not t.is_floating_point():
-            name = _TORCH_TYPE_NAMES.get(t.dtype, str(t.dtype))
-            raise RuntimeError(f"result type Float can't be cast to the desired output type {name}")
-        if t.dtype != torch.float32:
-            raise NotImplementedError(f"p2pdl_amd aggregates float32 state_dicts; {key} is {t.dtype}")
+    contiguous = _check_model(keys, ws, st)
 
-    ws = [state[key] for key in keys]
     if table is not None:
+        if contiguous:  # the validated model-state entry vouches for the pointers
+            ops.aggregate_ptr_table_(ws, table, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac,
+                                     w_ptrs=st.ptrs if st is not None else None,
+                                     numels=st.numels if st is not None else None)
+            _mark_rows_consumed(received)
+            logging.info(f"[{self.addr}:{self.port}] Model aggregation completed, applied local updates.")
+            self.received_models.clear()
+            broadcast_global_model_update(self)
+            return
         ws_c = [w if w.is_contiguous() else w.contiguous() for w in ws]
         ops.aggregate_ptr_table_(ws_c, table, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac)
         _mark_rows_consumed(received)
@@ -127,14 +132,33 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
     broadcast_global_model_update(self)
 
 
-def _gather_table(received, keys, state):
+def _check_model(keys, ws, st) -> bool:
+    """The reference raises at the division for integer tensors (:32);
+    float16 / float64 models are not aggregated here.  Returns whether every
+    model tensor is contiguous.  Decided once per validated model-state
+    entry (its tensors cannot change dtype or layout while it is valid)."""
+    done = st.extra.get("checked") if st is not None else None
+    if done is not None:
+        return done
+    for key, t in zip(keys, ws):
+        if not t.is_floating_point():
+            name = _TORCH_TYPE_NAMES.get(t.dtype, str(t.dtype))
+            raise RuntimeError(f"result type Float can't be cast to the desired output type {name}")
+        if t.dtype != torch.float32:
+            raise NotImplementedError(f"p2pdl_amd aggregates float32 state_dicts; {key} is {t.dtype}")
+    contiguous = all(t.is_contiguous() for t in ws)
+    if st is not None:
+        st.extra["checked"] = contiguous
+    return contiguous
+
+
+def _gather_table(received, keys, ws):
     """uint64 [L, K] device addresses of received[j]["model"][key], or None
     when the C gather cannot vouch for every tensor (not fp32 / contiguous /
     on the model's CUDA device / the parameter's element count) -- the
     caller's per-tensor path then diagnoses or widens exactly as before."""
     if _host_tables is None or not keys:
         return None
-    ws = [state[key] for key in keys]
     dev = ws[0].device
     if dev.type != "cuda":
         return None
@@ -159,7 +183,7 @@ def _checked_update(j, key, w, u):
     return u.contiguous()
 
 
-def _slab_fast_path(state, keys, received, rule, lr, trim_frac) -> bool:
+def _slab_fast_path(st, keys, ws, received, rule, lr, trim_frac) -> bool:
     """Updates landed by node.inbox.DeviceInbox (frozen LandedUpdate dicts
     whose fp32 tensors are rows of one device slab): the kernel table comes
     from (slab, rows, key offsets) in one broadcast -- no per-tensor Python
@@ -167,31 +191,38 @@ def _slab_fast_path(state, keys, received, rule, lr, trim_frac) -> bool:
     reference's error behaviour) unless every condition holds: all updates
     from one inbox, every model key a slab entry of every update, model
     tensors fp32 contiguous on the slab's device with the slab layout's
-    element counts."""
-    from ..node.inbox import LandedUpdate
-
+    element counts (decided once per (model state, inbox) when ``st``, the
+    validated model_state cache entry, is given)."""
     if not received:
         return False
     first = received[0].get("model") if isinstance(received[0], dict) else None
     if not isinstance(first, LandedUpdate):
         return False
     inbox = first.inbox
+    need = st.keyset if st is not None else frozenset(keys)
     for rm in received:
         u = rm.get("model") if isinstance(rm, dict) else None
-        if not isinstance(u, LandedUpdate) or u.inbox is not inbox or not u.slab_keys.issuperset(keys):
+        if not isinstance(u, LandedUpdate) or u.inbox is not inbox or not u.slab_keys >= need:
             return False
-    layout, dev = inbox.layout, inbox.slab.device
-    ws, offsets = [], []
-    for key in keys:
-        t = state[key]
-        off, _, n = layout[key]
-        if t.dtype != torch.float32 or t.device != dev or not t.is_contiguous() or t.numel() != n:
-            return False
-        ws.append(t)
-        offsets.append(off)
+    cached = st.extra.get("slab") if st is not None else None
+    if cached is not None and cached[0] is inbox:
+        offsets = cached[1]
+    else:
+        layout, dev = inbox.layout, inbox.slab.device
+        offsets = []
+        for key, t in zip(keys, ws):
+            off, _, n = layout[key]
+            if t.dtype != torch.float32 or t.device != dev or not t.is_contiguous() or t.numel() != n:
+                return False
+            offsets.append(off)
+        offsets = tuple(offsets)
+        if st is not None:
+            st.extra["slab"] = (inbox, offsets)
     inbox.order_after_landing()  # land()'s row copies ran on the listener thread's stream
     rows = [rm["model"].row for rm in received]
-    ops.aggregate_slab_rows_(ws, inbox.slab, rows, offsets, rule, lr=lr, trim_frac=trim_frac)
+    ops.aggregate_slab_rows_(ws, inbox.slab, rows, offsets, rule, lr=lr, trim_frac=trim_frac,
+                             w_ptrs=st.ptrs if st is not None else None,
+                             numels=st.numels if st is not None else None)
     inbox.slab_consumed()  # the next round's land() into these rows waits for this kernel
     return True
 
@@ -199,8 +230,6 @@ def _slab_fast_path(state, keys, received, rule, lr, trim_frac) -> bool:
 def _mark_rows_consumed(received) -> None:
     """General path over landed updates (e.g. mixed with plain dicts): each
     inbox learns that the launch just issued reads its rows."""
-    from ..node.inbox import LandedUpdate
-
     inboxes = {}
     for rm in received:
         u = rm.get("model") if isinstance(rm, dict) else None

@@ -834,13 +834,19 @@ class DeviceInbox:
         stream of the slab's device) reads slab rows: every later ``land``
         makes its own stream wait for that kernel before it overwrites a row
         (aggregation.py calls this after each launch over landed updates).
-        One event per consuming stream, re-recorded -- no allocation per call."""
-        stream = stream or torch.cuda.current_stream(self.device)
+        One event per consuming stream, re-recorded on raw handles -- no
+        allocation and no Stream object per call."""
+        from .. import _native as N
+
+        raw = stream.cuda_stream if stream is not None else N.stream_handle(self.device)
+        ev = self._consumers.get(raw)
+        if ev is not None:
+            N.event_record(ev.cuda_event, raw)
+            return
         with self._lock:
-            ev = self._consumers.get(stream.cuda_stream)
-            if ev is None:
-                ev = self._consumers[stream.cuda_stream] = torch.cuda.Event()
-            ev.record(stream)
+            ev = torch.cuda.Event()
+            ev.record(stream or torch.cuda.current_stream(self.device))
+            self._consumers[raw] = ev
 
     def _wait_rows_free(self, stream) -> None:
         for ev in self._consumers.values():  # under self._lock

@@ -294,14 +294,16 @@ def aggregate_segments_(ws: Sequence[torch.Tensor], peer_lists: Sequence[Sequenc
 
 
 def aggregate_ptr_table_(ws: Sequence[torch.Tensor], ptrs: np.ndarray, rule="fedavg", *, lr: float = 0.1,
-                         trim_b: int | None = None, trim_frac: float = DEFAULT_TRIM_FRAC) -> None:
+                         trim_b: int | None = None, trim_frac: float = DEFAULT_TRIM_FRAC,
+                         w_ptrs: tuple | None = None, numels: tuple | None = None) -> None:
     """aggregate_segments_ for a peer-pointer table the caller has already
     gathered and validated: ptrs[l, j] = device address of update j's
     fp32 tensor for key l (ws[l].numel() elements each, contiguous, on ws'
     device) -- what _host_tables.gather_peer_table returns for
     aggregate_models' general path.  The device table is cached by the
     addresses and sizes it encodes (a round whose updates land at the same
-    addresses reuses it, as aggregate_slab_rows_ does)."""
+    addresses reuses it, as aggregate_slab_rows_ does).  ``w_ptrs`` /
+    ``numels``: caller-validated, as for aggregate_slab_rows_."""
     L = len(ws)
     if L == 0:
         return
@@ -310,12 +312,13 @@ def aggregate_ptr_table_(ws: Sequence[torch.Tensor], ptrs: np.ndarray, rule="fed
     K = ptrs.shape[1]
     dev = ws[0].device
     N.require_device(ws[0])
-    numels = []
-    for l, w in enumerate(ws):
-        _check_f32(w, f"w[{l}]", dev)
-        numels.append(w.numel())
-    key = (dev.index, "ptrs", ptrs.tobytes(), tuple(w.data_ptr() for w in ws), tuple(numels), rule_id(rule), K,
-           trim_b, float(trim_frac))
+    if w_ptrs is None:
+        for l, w in enumerate(ws):
+            _check_f32(w, f"w[{l}]", dev)
+        w_ptrs = tuple(w.data_ptr() for w in ws)
+    if numels is None:
+        numels = tuple(w.numel() for w in ws)
+    key = (dev.index, "ptrs", ptrs.tobytes(), w_ptrs, numels, rule_id(rule), K, trim_b, float(trim_frac))
     with _TABLES_LOCK:
         hit = _TABLES.get(key)
         if hit is not None:
@@ -333,27 +336,33 @@ def aggregate_ptr_table_(ws: Sequence[torch.Tensor], ptrs: np.ndarray, rule="fed
 
 def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: Sequence[int],
                          offsets: Sequence[int], rule="fedavg", *, lr: float = 0.1,
-                         trim_b: int | None = None, trim_frac: float = DEFAULT_TRIM_FRAC) -> None:
+                         trim_b: int | None = None, trim_frac: float = DEFAULT_TRIM_FRAC,
+                         w_ptrs: tuple | None = None, numels: tuple | None = None) -> None:
     """aggregate_segments_ for updates that are rows of one [K_max, N] fp32
     slab (what node.inbox.DeviceInbox lands): update j's tensor for key l is
     slab[rows[j], offsets[l] : offsets[l] + ws[l].numel()].  The (L, K) peer
-    table is computed with one broadcast instead of inspecting L*K tensors."""
+    table is computed with one broadcast instead of inspecting L*K tensors.
+    ``w_ptrs``: the ws' data pointers, from a caller that has already checked
+    ws (fp32, contiguous, on the slab's device) and vouches they are
+    unchanged (aggregation.py's validated model-state cache); the per-tensor
+    checks are then skipped (``numels``: their element counts, likewise)."""
     L, K = len(ws), len(rows)
     if L == 0:
         return
     if K == 0:
         raise ValueError("need at least one peer update")
-    dev = ws[0].device
-    N.require_device(ws[0])
-    _check_f32(slab, "slab", dev)
-    if slab.dim() != 2:
-        raise ValueError("slab must be [K_max, N]")
-    numels = []
-    for l, w in enumerate(ws):
-        _check_f32(w, f"w[{l}]", dev)
-        numels.append(w.numel())
-    key = (dev.index, slab.data_ptr(), slab.shape[0], slab.shape[1], slab.stride(0), tuple(rows), tuple(offsets),
-           tuple(w.data_ptr() for w in ws), tuple(numels), rule_id(rule), K, trim_b, float(trim_frac))
+    dev = slab.device
+    N.require_device(slab)
+    if slab.dtype != torch.float32 or slab.dim() != 2 or not slab.is_contiguous():
+        raise ValueError("slab must be a contiguous fp32 [K_max, N] tensor")
+    if w_ptrs is None:
+        for l, w in enumerate(ws):
+            _check_f32(w, f"w[{l}]", dev)
+        w_ptrs = tuple(w.data_ptr() for w in ws)
+    if numels is None:
+        numels = tuple(w.numel() for w in ws)
+    key = (dev.index, slab.data_ptr(), slab.shape[0], slab.shape[1], tuple(rows), tuple(offsets),
+           w_ptrs, numels, rule_id(rule), K, trim_b, float(trim_frac))
     with _TABLES_LOCK:
         hit = _TABLES.get(key)
         if hit is not None:
@@ -373,7 +382,7 @@ def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: S
         raise IndexError("slab row out of range")
     if offs_a.min() < 0 or (offs_a + np.asarray(numels, dtype=np.int64)).max() > width:
         raise IndexError("segment outside the slab row")
-    base, stride = slab.data_ptr(), slab.stride(0) * 4
+    base, stride = slab.data_ptr(), width * 4
     ptrs = (np.uint64(base) + rows_a.astype(np.uint64)[None, :] * np.uint64(stride)
             + offs_a.astype(np.uint64)[:, None] * np.uint64(4))
     _launch_segments(ws, ptrs, numels, rule, K, lr, trim_b, trim_frac, None, dev, cache_key=key)

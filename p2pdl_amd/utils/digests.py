@@ -214,10 +214,19 @@ def digest_async(data) -> Future:
     return fut
 
 
-# Below this many distinct uncached messages the host threads win; at and
-# above it the GPU batch kernel does (one lane chain per message, so many
-# short messages; measured boundary).
-GPU_BATCH_MIN = 2048
+# The GPU batch kernel hashes every message on its own lane chain (~33 MB/s
+# each, all in parallel); the host hashes one message per thread at ~2.4
+# GB/s (SHA-NI).  For host-resident messages the GPU wins only for a batch of
+# many short ones (measured boundary, DESIGN.md §3 K3,
+# profiles/r04/digest_boundary.json): at least GPU_BATCH_MIN distinct
+# messages, none longer than GPU_MAX_MESSAGE bytes.
+GPU_BATCH_MIN = 256
+GPU_MAX_MESSAGE = 16384
+HOST_THREAD_MIN = 1 << 16  # shorter messages hash inline on the calling thread
+
+
+def _gpu_batch_wins(msgs) -> bool:
+    return len(msgs) >= GPU_BATCH_MIN and max(len(m) for m in msgs) <= GPU_MAX_MESSAGE
 
 
 def digest_many(messages) -> list:
@@ -253,14 +262,19 @@ def digest_many(messages) -> list:
             slot[i] = j
         with CACHE._lock:
             CACHE.misses += len(uniq)
-        if len(uniq) >= GPU_BATCH_MIN:
+        if _gpu_batch_wins(uniq):
             from .. import ops
 
             ds = ops.sha256_batch(uniq)
-        elif len(uniq) == 1:
-            ds = [sha256_host(uniq[0])]
-        else:
-            ds = list(hash_pool().map(sha256_host, uniq))
+        else:  # long messages on the hashing threads, short ones inline (a task costs ~20 us)
+            big = [j for j, m in enumerate(uniq) if len(m) >= HOST_THREAD_MIN]
+            ds = [None] * len(uniq)
+            if len(big) > 1:
+                for j, d in zip(big, hash_pool().map(sha256_host, [uniq[j] for j in big])):
+                    ds[j] = d
+            for j, m in enumerate(uniq):
+                if ds[j] is None:
+                    ds[j] = sha256_host(m)
         for i in todo:
             out[i] = ds[slot[i]]
             CACHE.put(messages[i], out[i])

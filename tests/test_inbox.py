@@ -740,8 +740,8 @@ def test_pinned_landing_concurrent_listeners(cuda):
     def worker(j):
         barrier.wait()
         for _ in range(3):  # reuse pooled buffers while others land
-            m = _pinned(inbox, ser[j])
-            got[j] = inbox.land(m, j)
+            with _pinned(inbox, ser[j]) as m:  # released as the listener's frame ends
+                got[j] = inbox.land(m, j)
 
     ths = [threading.Thread(target=worker, args=(j,)) for j in range(k)]
     for th in ths:
