@@ -243,6 +243,7 @@ def test_gpu_digests_match_hashlib_with_dedupe(cuda, monkeypatch):
     real = ops.sha256_batch
     monkeypatch.setattr(ops, "sha256_batch", lambda m, device=None: calls.append(len(m)) or real(m, device))
     monkeypatch.setattr(digests, "GPU_BATCH_MIN", 2)
+    monkeypatch.setattr(digests, "GPU_MAX_MESSAGE", 1 << 30)
     digests.CACHE.clear()
     updates = [pickle.dumps({"t": t, "w": bytes(range(256)) * (1000 + 37 * t)}) for t in range(3)]
     msgs = [u for _ in range(24) for u in updates]
