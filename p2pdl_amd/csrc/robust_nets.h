@@ -32,14 +32,41 @@ __device__ __forceinline__ uint64_t unordered_mask(float a, float b) {
   return m;
 }
 
+// Lanes for which any of the N values at(0) .. at(N-1) is NaN.  NaN
+// propagates through v_pk_fma_f32 (a * b + c on float pairs), so each
+// instruction folds four more values into a running pair: the first takes
+// six, the rest four, and one v_cmp_u_f32 tests the final pair -- about N/4 + 1
+// instructions where one compare per two values takes N/2 (the loaded
+// values already sit in register pairs: no moves).  An overflowing product,
+// inf * 0 or inf - inf also ends in NaN: a false alarm only sends the tile
+// to the exact uint32-key network.  Fewer than six values: compares.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) {
+  f2v d;
+  asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+template <int N, typename F>
+__device__ __forceinline__ uint64_t nan_lanes(F&& at) {
+  static_assert(N % 2 == 0, "pairs");
+  if constexpr (N < 6) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int j = 0; j < N / 2; ++j) m |= unordered_mask(at(j), at(j + N / 2));
+    return m;
+  } else {
+    f2v acc = pk_fma(f2v{at(0), at(1)}, f2v{at(2), at(3)}, f2v{at(4), at(5)});
+#pragma unroll
+    for (int j = 6; j + 3 < N; j += 4) acc = pk_fma(f2v{at(j), at(j + 1)}, f2v{at(j + 2), at(j + 3)}, acc);
+    if constexpr ((N - 6) % 4 == 2) acc = pk_fma(f2v{at(N - 2), at(N - 1)}, f2v{1.f, 1.f}, acc);
+    return unordered_mask(acc.x, acc.y);
+  }
+}
+
 // Any NaN among the n values of any lane of the wave (wave-uniform).
 template <int N>
 __device__ __forceinline__ bool wave_has_nan(const uint32_t (&bits)[N]) {
-  static_assert(N % 2 == 0, "pairs");
-  uint64_t m = 0;
-#pragma unroll
-  for (int j = 0; j < N / 2; ++j) m |= unordered_mask(__uint_as_float(bits[j]), __uint_as_float(bits[j + N / 2]));
-  return m != 0;
+  return nan_lanes<N>([&](int j) { return __uint_as_float(bits[j]); }) != 0;
 }
 
 template <bool ASC, typename T>
@@ -86,8 +113,8 @@ struct NoHook {
 __device__ __forceinline__ float bits_f(uint32_t k) { return __uint_as_float(k); }
 __device__ __forceinline__ float bits_f(fk x) { return x.x; }
 __device__ __forceinline__ float bits_f(fx x) { return x.x; }
-// The NaN test of the float networks, one v_cmp_u_f32 per two keys, block by
-// block as the network first reads it: the compares wait only for that
+// The NaN test of the float networks (nan_lanes: packed FMAs), block by
+// block as the network first reads it: the test waits only for that
 // block's loads (a whole-wave test up front waited for every load before the
 // first comparator: median256 -3.5% time without it).
 // G blocks per test, blocks from FIRST on.
@@ -98,8 +125,7 @@ struct NanHook {
   __device__ __forceinline__ void operator()(T (&v)[KP], int blk) const {
     if (blk % G != 0 || blk < FIRST) return;
     constexpr int N = 16 * G < KP ? 16 * G : KP;
-#pragma unroll
-    for (int j = 0; j < N / 2; ++j) m |= unordered_mask(bits_f(v[16 * blk + j]), bits_f(v[16 * blk + N / 2 + j]));
+    m |= nan_lanes<N>([&](int j) { return bits_f(v[16 * blk + j]); });
   }
 };
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {

@@ -110,13 +110,10 @@ __device__ __forceinline__ void pin(const T (&x)[N]) {
   for (int j = 0; j < N; ++j) asm volatile("" ::"v"(raw(x[j])));
 }
 
-// NaN test of N consecutive loaded keys (one v_cmp_u_f32 per two).
+// NaN test of N consecutive loaded keys (robust_nets.h nan_lanes).
 template <int N>
 __device__ __forceinline__ uint64_t list_nan_mask(const uint32_t* v) {
-  uint64_t m = 0;
-#pragma unroll
-  for (int j = 0; j < N / 2; ++j) m |= unordered_mask(__uint_as_float(v[j]), __uint_as_float(v[j + N / 2]));
-  return m;
+  return nan_lanes<N>([&](int j) { return __uint_as_float(v[j]); });
 }
 
 // One half sorted in T's domain (the block's: keys if either half holds a

@@ -457,6 +457,34 @@ def test_robust_float_fast_path_specials(cuda, rule, k, nan_stripe):
     assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k} nan={nan_stripe}")
 
 
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+@pytest.mark.parametrize("k", [16, 64, 128, 200, 256])
+def test_robust_single_nan_at_every_peer_position(cuda, rule, k):
+    """The float networks' NaN test (robust_nets.h nan_lanes: packed-FMA
+    chains ended by one compare) must see a NaN wherever it sits: tile t
+    (64 coordinates, one wave / pair block) holds exactly one NaN, at peer t,
+    in lane 7t mod 64 -- every peer position of every chain is hit once, with
+    both signs and a payload -- among values whose products overflow in other
+    tiles (false alarms only take the exact key path).  Bit-exact vs the
+    oracle."""
+    n = 64 * k
+    peers = [oracle.synth(n, 77 + k, p, 1e-2) for p in range(k)]
+    nans = np.array([0x7FC00000, 0xFFC00000, 0x7F800001, 0xFFBFFFFF], dtype=np.uint32).view(np.float32)
+    for t in range(k):
+        peers[t][64 * t + (7 * t) % 64] = nans[t % 4]
+    big = np.float32(3e38)
+    for p in range(0, k, 3):  # products that overflow (no NaN): a false alarm at most
+        peers[p][64 * ((p + 1) % k) + 63] = big if p % 2 else -big
+    w = oracle.synth(n, 6, 0xFFFFF, 5e-2)
+    r = ops.rule_id(rule)
+    b = ops.trim_count(k) if rule == "trimmed" else 0
+    w_ref, out_ref = oracle.robust(peers, r, b, w=w)
+    wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate([to_dev(p, cuda) for p in peers], rule, w=wt, out=out, trim_b=b)
+    assert_bits_equal(host(out), out_ref, nan_equal=(rule != "median"), what=f"{rule} K={k} one NaN per tile")
+    assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k} one NaN per tile")
+
+
 @pytest.mark.parametrize("k,b", [(5, 0), (5, 2), (10, 3), (128, 0), (128, 63), (200, 10), (256, 51), (256, 100)])
 def test_trimmed_explicit_b(cuda, k, b):
     n = 1000

@@ -7,8 +7,9 @@ still a specified input class: a wave (or pair block) holding one must take
 the uint32-key network.  These checks read the code object inside
 p2pdl_amd/libp2pdl_hip.so (llvm-objdump, tools/isa_stats.py) and assert
   * every function that runs the float network also issues the explicit NaN
-    test (v_cmp_u_f32, at least one per two keys it loads) -- the compiler
-    would fold an isnan() away under this flag, an asm compare it cannot;
+    test over every key it loads (asm v_pk_fma_f32 chains, through which NaN
+    propagates, ended by a v_cmp_u_f32; or one compare per two keys) -- the
+    compiler would fold an isnan() away under this flag, asm it cannot;
   * every key-path function (pair_keys, robust_coord_keys) and every MODE 0
     kernel sorts with integer min / max / med3 only, so a NaN key is ranked
     by its bits whatever the float mode;
@@ -69,10 +70,14 @@ def test_float_network_always_behind_the_nan_test(funcs):
             continue
         if _count(c, FLOAT_MINMAX) == 0:
             continue
-        nan_tests = c["v_cmp_u_f32"] + c["v_cmp_u_f32_e64"] + c["v_cmp_u_f32_e32"]
-        # the loads of the function: one per key (pair: 128 per wave, K <= 128: KP)
+        cmps = c["v_cmp_u_f32"] + c["v_cmp_u_f32_e64"] + c["v_cmp_u_f32_e32"]
+        pk = c["v_pk_fma_f32"]
+        # the loads of the function: one per key (pair: 128 per wave, K <= 128: KP).
+        # robust_nets.h nan_lanes: a chain of packed FMAs folds 6 keys, then 4
+        # per instruction, into a pair that one compare tests; plain compares
+        # test 2 keys each -- either way 4 * pk + 2 * cmps keys are covered
         loads = sum(v for k, v in c.items() if k.startswith("global_load") and "lds" not in k)
-        assert nan_tests >= loads // 2 > 0, (name, nan_tests, loads)
+        assert cmps > 0 and 4 * pk + 2 * cmps >= loads > 0, (name, cmps, pk, loads)
         checked += 1
     assert checked >= 6
 
