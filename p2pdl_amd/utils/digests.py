@@ -113,6 +113,8 @@ class DigestCache:
         if isinstance(data, bytes):
             ref = data
         elif _is_window(data):
+            if not data._held:
+                return
             oid0 = id(data)
 
             def gone(_, oid=oid0, cache=self):
@@ -146,13 +148,15 @@ class DigestCache:
             if not bucket:
                 return None
             ent = bucket.get(oid)
-            if ent is not None and self._alive(ent[0]) is data:
+            if ent is not None and self._alive(ent[0]) is data and not (_is_window(data) and not data._held):
                 self._by_id.move_to_end(oid)
                 self.hits_identity += 1
                 return ent[1]
             cands = [(self._alive(r), d) for r, d in bucket.values()]
         for obj, d in cands:
-            if obj is not None and _same_bytes(mv, _buffer(obj)):
+            if obj is None or (_is_window(obj) and not obj._held):
+                continue  # a released window: its buffer may hold another message by now
+            if _same_bytes(mv, _buffer(obj)):
                 with self._lock:
                     self.hits_content += 1
                 self.put(data, d)  # the next lookup of this object is by identity

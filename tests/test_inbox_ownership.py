@@ -286,3 +286,17 @@ def test_payload_outside_the_message_is_refused(cuda):
     with pytest.raises(pickle.UnpicklingError):
         with inbox._lock:
             inbox._land_pinned_locked(m, raw, 0)
+
+
+def test_released_window_never_answers_a_digest_lookup(pageable):
+    """A window's cache entry stops counting once the window is released: its
+    buffer may already hold another peer's message."""
+    digests.CACHE.clear()
+    ser = pickle.dumps({"w": torch.arange(64, dtype=torch.float32)})
+    w = open_envelope(message(pageable, pickle.dumps({"type": "model_update", "model": ser,
+                                                       "addr": "a", "port": 1})))["model"]
+    d = digests.digest_of(w)
+    w.release()
+    assert digests.CACHE.get(bytes(ser)) is None  # no content hit through the released window
+    assert digests.digest_of(bytes(ser)) == d == hashlib.sha256(ser).digest()
+    digests.CACHE.clear()
