@@ -40,7 +40,7 @@ import os
 import pickle
 import struct
 import threading
-from collections import OrderedDict
+from collections import OrderedDict, deque
 from dataclasses import dataclass
 
 import numpy as np
@@ -571,7 +571,7 @@ class PinnedMessage:
             raise ValueError("window outside the message")
         return PinnedMessage(self.root, at, len(part))
 
-    def release(self) -> None:
+    def release(self, _collected: bool = False) -> None:
         """Give this handle up (idempotent)."""
         with _REF_LOCK:
             if not self._held:
@@ -580,7 +580,13 @@ class PinnedMessage:
             self.root.refs -= 1
             last = self.root.refs == 0
         if last and self.root.pool is not None:
-            self.root.pool._release(self.root)
+            if _collected:
+                # from __del__: the garbage collector can run this on a thread
+                # that holds the inbox's lock, so no lock here -- the buffer
+                # is queued and the pool takes it at its next hand-out
+                self.root.pool._return_later(self.root)
+            else:
+                self.root.pool._release(self.root)
 
     def __enter__(self):
         return self
@@ -591,7 +597,7 @@ class PinnedMessage:
 
     def __del__(self):
         try:
-            self.release()
+            self.release(_collected=True)
         except Exception:  # interpreter shutdown
             pass
 
@@ -727,6 +733,7 @@ class DeviceInbox:
                                      4 * self.row + extra + 1024 * len(template) + (1 << 20))
         self.pool_bytes = int(pool_bytes if pool_bytes is not None else 2 * self.k_max * self.max_message_bytes)
         self._pinned_free = []     # _PinnedBuffer pool
+        self._returned = deque()   # buffers of finalised handles, pooled at the next hand-out
         self._consumers = {}       # stream handle -> event after its last kernel over the slab
         self._digests = {}
         self.count = 0
@@ -792,6 +799,7 @@ class DeviceInbox:
         to the pool when the handle and every window of it are released."""
         nbytes = int(nbytes)
         with self._lock:
+            self._drain_returned_locked()
             fits = [p for p in self._pinned_free if p.capacity >= nbytes]
             root = min(fits, key=lambda p: p.capacity) if fits else None
             if root is not None:
@@ -805,10 +813,22 @@ class DeviceInbox:
         """A buffer with no live handle: back to the pool while the pool holds
         at most pool_bytes, freed otherwise."""
         with self._lock:
-            if any(p is root for p in self._pinned_free):
-                return
-            if sum(p.capacity for p in self._pinned_free) + root.capacity <= self.pool_bytes:
-                self._pinned_free.append(root)
+            self._pool_locked(root)
+
+    def _pool_locked(self, root: _PinnedBuffer) -> None:
+        if any(p is root for p in self._pinned_free):
+            return
+        if sum(p.capacity for p in self._pinned_free) + root.capacity <= self.pool_bytes:
+            self._pinned_free.append(root)
+
+    def _return_later(self, root: _PinnedBuffer) -> None:
+        """_release without the lock (deque.append is atomic): for handles
+        the garbage collector finalises."""
+        self._returned.append(root)
+
+    def _drain_returned_locked(self) -> None:
+        while self._returned:
+            self._pool_locked(self._returned.popleft())
 
     def recv(self, conn):
         """``recv_message`` into a pinned buffer of this inbox: the 4-byte

@@ -33,7 +33,7 @@ import hashlib
 import os
 import threading
 import weakref
-from collections import OrderedDict
+from collections import OrderedDict, deque
 from concurrent.futures import Future
 
 import numpy as np
@@ -76,6 +76,7 @@ class DigestCache:
         self._by_id: "OrderedDict[int, tuple]" = OrderedDict()  # id -> (ref, key)
         self._by_key: dict = {}  # content key -> {id: (ref, digest or Future)}
         self._held = 0  # bytes of strongly held `bytes` objects
+        self._dead = deque()  # weak references whose windows died
         self._lock = threading.Lock()
         self.hits_identity = self.hits_content = self.misses = 0
 
@@ -90,12 +91,23 @@ class DigestCache:
 
     def clear(self) -> None:
         with self._lock:
+            self._dead.clear()
             self._by_id.clear()
             self._by_key.clear()
             self._held = 0
 
     def __len__(self) -> int:
-        return len(self._by_id)
+        with self._lock:
+            self._purge_locked()
+            return len(self._by_id)
+
+    def _purge_locked(self) -> None:
+        while self._dead:
+            ref = self._dead.popleft()
+            for oid, (r, _) in list(self._by_id.items()):
+                if r is ref:
+                    self._drop_locked(oid)
+                    break
 
     def _drop_locked(self, oid: int) -> None:
         ref, key = self._by_id.pop(oid)
@@ -115,20 +127,15 @@ class DigestCache:
         elif _is_window(data):
             if not data._held:
                 return
-            oid0 = id(data)
-
-            def gone(_, oid=oid0, cache=self):
-                with cache._lock:
-                    ent = cache._by_id.get(oid)
-                    if ent is not None and isinstance(ent[0], weakref.ref) and ent[0]() is None:
-                        cache._drop_locked(oid)
-
-            ref = weakref.ref(data, gone)
+            # the entry is purged lazily: the callback may run (garbage
+            # collection) on a thread inside this cache's lock
+            ref = weakref.ref(data, self._dead.append)
         else:
             return  # mutable: looked up, never kept
         key = self._key(_buffer(data))
         oid = id(data)
         with self._lock:
+            self._purge_locked()
             if oid in self._by_id:
                 self._drop_locked(oid)
             self._by_id[oid] = (ref, key)
@@ -144,6 +151,7 @@ class DigestCache:
         mv = _buffer(data)
         key = self._key(mv)
         with self._lock:
+            self._purge_locked()
             bucket = self._by_key.get(key)
             if not bucket:
                 return None

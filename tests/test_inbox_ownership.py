@@ -36,6 +36,8 @@ class FakePool:
     def _release(self, root):
         self.back.append(root)
 
+    _return_later = _release  # the finaliser's lock-free path
+
 
 @pytest.fixture
 def pageable(monkeypatch):
@@ -114,12 +116,13 @@ def test_other_envelopes_decode_like_the_reference(pageable, kind):
 
 
 def test_pool_is_bounded_by_bytes():
-    pool = types.SimpleNamespace(_lock=threading.Lock(), _pinned_free=[], pool_bytes=1000)
+    pool = DeviceInbox.__new__(DeviceInbox)  # the pool's state only
+    pool._lock, pool._pinned_free, pool.pool_bytes = threading.Lock(), [], 1000
     roots = [types.SimpleNamespace(capacity=c) for c in (400, 400, 400, 100)]
     for r in roots:
-        DeviceInbox._release(pool, r)
+        pool._release(r)
     assert pool._pinned_free == [roots[0], roots[1], roots[3]]  # the third 400 would exceed 1000
-    DeviceInbox._release(pool, roots[0])  # idempotent
+    pool._release(roots[0])  # idempotent
     assert len(pool._pinned_free) == 3
 
 
@@ -300,3 +303,31 @@ def test_released_window_never_answers_a_digest_lookup(pageable):
     assert digests.CACHE.get(bytes(ser)) is None  # no content hit through the released window
     assert digests.digest_of(bytes(ser)) == d == hashlib.sha256(ser).digest()
     digests.CACHE.clear()
+
+
+def test_finalised_handle_takes_no_lock(pageable):
+    """A handle the garbage collector finalises while this thread holds the
+    inbox's lock (a cycle collected inside land()) must not deadlock: the
+    finaliser queues the buffer and the next hand-out pools it."""
+    inbox = DeviceInbox.__new__(DeviceInbox)
+    inbox._lock, inbox._pinned_free, inbox._returned, inbox.pool_bytes = (threading.Lock(), [],
+                                                                          collections.deque(), 1 << 20)
+    root = _PinnedBuffer(64, inbox)
+    m = PinnedMessage(root, 0, 64)
+    with inbox._lock:
+        m.__del__()  # what collection inside the locked region runs
+    assert list(inbox._returned) == [root] and inbox._pinned_free == []
+    with inbox._lock:
+        inbox._drain_returned_locked()
+    assert inbox._pinned_free == [root]
+
+
+def test_window_death_inside_the_cache_lock_does_not_deadlock(pageable):
+    digests.CACHE.clear()
+    ser = pickle.dumps({"w": torch.zeros(8)})
+    w = open_envelope(message(pageable, pickle.dumps({"type": "model_update", "model": ser, "addr": "a",
+                                                       "port": 1})))["model"]
+    digests.digest_of(w)
+    with digests.CACHE._lock:
+        del w  # the weak reference's callback runs here, inside the lock
+    assert len(digests.CACHE) == 0
