@@ -429,6 +429,12 @@ def _is_tensor_dict(obj) -> bool:
     return isinstance(obj, dict) and all(isinstance(v, RawTensor) for v in dict.values(obj))
 
 
+try:  # the same machine in C++ (csrc/wire.cpp), built beside the HIP library
+    from .. import _wire
+except ImportError:
+    _wire = None
+
+
 class ZeroCopyParser:
     """Reader for the pickled state_dict of a peer update (reference
     node/node.py:285; pickle protocols 3-5).  Runs the restricted stack
@@ -436,12 +442,25 @@ class ZeroCopyParser:
     tensor payloads are never copied -- only the three globals above resolve,
     and anything else, or any malformed byte, raises
     ``pickle.UnpicklingError`` (so a listener that catches only that cannot
-    be killed by a peer's bytes)."""
+    be killed by a peer's bytes).
 
-    def __init__(self, data):
+    ``native`` (default: when built) runs the machine in C++
+    (``csrc/wire.cpp``, without the GIL) -- the same opcodes, globals and
+    checks as the Python machine below, which the tests hold it to; it
+    returns the same RawTensor / RawStorage views."""
+
+    def __init__(self, data, native: bool | None = None):
         self.mv = memoryview(data).cast("B")
+        self.native = (_wire is not None) if native is None else native
+        if self.native and _wire is None:
+            raise ImportError("p2pdl_amd._wire is not built (make -C p2pdl_amd/csrc)")
 
     def parse(self) -> dict:
+        if self.native:
+            entries, storages = _wire.parse_update(self.mv)
+            mv = self.mv
+            st = [RawStorage(_STORAGE_DTYPES[t], numel, mv[off:off + nb], loc) for t, numel, off, nb, loc in storages]
+            return OrderedDict((key, RawTensor(st[si], o, size, stride)) for key, si, o, size, stride in entries)
         try:
             obj, _ = _run_pickle(self.mv, 0, min_proto=3, resolve_global=_update_global)
         except pickle.UnpicklingError:

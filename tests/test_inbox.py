@@ -40,10 +40,11 @@ def same(raw, ref):
         assert a.dtype == r.dtype and np.array_equal(a.view(np.uint8), r.view(np.uint8)), k
 
 
-PARSERS = [lambda d: ZeroCopyParser(d).parse()]
+# the Python machine and its C++ port (csrc/wire.cpp) on every case
+PARSERS = [lambda d: ZeroCopyParser(d, native=False).parse(), lambda d: ZeroCopyParser(d, native=True).parse()]
 
 
-@pytest.mark.parametrize("parse", PARSERS, ids=["zero-copy"])
+@pytest.mark.parametrize("parse", PARSERS, ids=["python", "native"])
 def test_parser_matches_pickle_loads_mlp_update(parse):
     upd = mlp_update(1)
     data = pickle.dumps(upd)  # reference node/node.py:285
@@ -51,7 +52,7 @@ def test_parser_matches_pickle_loads_mlp_update(parse):
 
 
 @pytest.mark.parametrize("proto", [3, 4, 5])
-@pytest.mark.parametrize("parse", PARSERS, ids=["zero-copy"])
+@pytest.mark.parametrize("parse", PARSERS, ids=["python", "native"])
 def test_parser_batchnorm_scalars_views_and_ordereddict(parse, proto):
     net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.BatchNorm1d(5))
     sd = net.state_dict()  # OrderedDict incl. an int64 0-d buffer
@@ -60,6 +61,14 @@ def test_parser_batchnorm_scalars_views_and_ordereddict(parse, proto):
     sd["x" * 300] = torch.ones(3)                                           # BINUNICODE key
     data = pickle.dumps(sd, protocol=proto)
     same(parse(data), pickle.loads(data))
+
+
+def test_native_parser_is_the_default():
+    """The receive path runs the C++ machine (csrc/wire.cpp) when it is built
+    -- __graft_entry__.build() builds it beside the HIP library."""
+    from p2pdl_amd import _wire  # noqa: F401
+
+    assert ZeroCopyParser(b"").native is True
 
 
 def test_zero_copy_parser_payloads_alias_the_message():
