@@ -124,6 +124,31 @@ def test_parsers_raise_only_unpickling_error_on_corrupted_bytes():
                 pass
 
 
+def test_native_and_python_machines_agree_on_corrupted_bytes():
+    """Differential fuzz of the two machines: on every corruption both reject,
+    or both accept with the same keys, dtypes, views and payload bytes."""
+    rng = np.random.default_rng(7)
+    data = pickle.dumps(torch.nn.Sequential(torch.nn.Linear(3, 2), torch.nn.BatchNorm1d(2)).state_dict())
+
+    def run(native, d):
+        try:
+            r = ZeroCopyParser(d, native=native).parse()
+        except pickle.UnpicklingError:
+            return None
+        return [(k, v.storage.dtype, v.storage.numel, v.storage.location, v.offset, v.size, v.stride,
+                 bytes(v.storage.data)) for k, v in r.items()]
+
+    accepted = 0
+    for _ in range(3000):
+        m = bytearray(data)
+        for i in rng.integers(0, len(m), rng.integers(1, 4)):
+            m[i] = int(rng.integers(0, 256))
+        a, b = run(False, bytes(m)), run(True, bytes(m))
+        assert a == b, bytes(m)
+        accepted += a is not None
+    assert accepted > 0  # some corruptions hit payload bytes only
+
+
 # ---- forged updates: the storage blob and the tensor view come from the peer
 def _good_blob(n=2):
     import warnings
