@@ -26,6 +26,7 @@ Build extensions (keyword-only, defaults reproduce the reference): ``rule``
 import logging
 import pickle
 import socket
+import weakref
 
 import numpy as np
 import torch
@@ -205,7 +206,7 @@ def _slab_fast_path(st, keys, ws, received, rule, lr, trim_frac) -> bool:
         if not isinstance(u, LandedUpdate) or u.inbox is not inbox or not u.slab_keys >= need:
             return False
     cached = st.extra.get("slab") if st is not None else None
-    if cached is not None and cached[0] is inbox:
+    if cached is not None and cached[0]() is inbox:  # a weak reference: the cache keeps no inbox alive
         offsets = cached[1]
     else:
         layout, dev = inbox.layout, inbox.slab.device
@@ -217,7 +218,7 @@ def _slab_fast_path(st, keys, ws, received, rule, lr, trim_frac) -> bool:
             offsets.append(off)
         offsets = tuple(offsets)
         if st is not None:
-            st.extra["slab"] = (inbox, offsets)
+            st.extra["slab"] = (weakref.ref(inbox), offsets)
     inbox.order_after_landing()  # land()'s row copies ran on the listener thread's stream
     rows = [rm["model"].row for rm in received]
     ops.aggregate_slab_rows_(ws, inbox.slab, rows, offsets, rule, lr=lr, trim_frac=trim_frac,

@@ -47,9 +47,8 @@ _PROBE = 32  # bytes of head and tail in the content key
 
 def _buffer(data) -> memoryview:
     """Byte view of bytes / bytearray / memoryview / PinnedMessage."""
-    view = getattr(data, "view", None)
-    if callable(view) and not isinstance(data, memoryview):
-        return view()
+    if _is_window(data):
+        return data.view()
     return memoryview(data).cast("B")
 
 
