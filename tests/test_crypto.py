@@ -260,3 +260,16 @@ def test_module_exports_what_the_reference_imports():
     for name in ("KeyServer", "generate_key_pair", "verify_signature", "verify_signature_2", "sign_data"):
         assert name in ns, name
     assert ns["verify_signature_2"](None, "a", 1, b"x", b"s") is True  # reference :61-62
+
+
+def test_bench_digest_flow_record_on_cpu():
+    """bench.py's digest_flow record (the reference's per-round 72 sign /
+    verify digests over 3 MLP updates) runs on the host: the
+    product hashes 3 times and every signature is over hashlib's digest."""
+    import bench
+
+    rec = bench.run_digest_flow(None, 1)
+    cfg = rec["config"]
+    assert cfg["hashes_product"] == 3 and cfg["hashes_reference"] == 72
+    assert cfg["message_bytes"] > 2_000_000 and rec["ms_per_step"] > 0
+    assert len(digests.CACHE) == 0  # the record leaves the process cache empty
