@@ -31,6 +31,10 @@ Sub-records (the "sub" object of the same line):
   inbox         16 serialized ResNet-18 updates landed in the device slab
                 (vs the reference's pickle.loads), with the echo digest
                 overlapped
+  digest_flow   the reference's per-round 72 sign / verify digests through
+                crypto.sign_data / verify_signature (vs 72 hashlib passes)
+  broadcast     the global model's envelope pickled from the GPU (one D2H
+                transfer) vs the reference's pickle of the CUDA state_dict
 (N = 1 only, except cfg3_full, which runs at every N.)
 
 roofline.achieved = algorithmic bytes per launch 4n(K+2) / mean kernel time
@@ -84,13 +88,15 @@ WORKLOADS = {
     # land 16 serialized ResNet-18-sized updates (11.7M
     # params each) in the device slab vs the reference's pickle.loads
     "inbox": ("inbox", 16, 11_689_512, 0x5EED0007),
+    # the global model pickled for the broadcast
+    "broadcast": ("broadcast", 1, 11_689_512, 0x5EED0008),
     # the reference's per-round digest work: 72 sign/verify hashes over 3 MLP
     # updates, through crypto.sign_data / verify_signature
     "digest-flow": ("digest-flow", 3, 535_818, 0),
 }
 SUB_N1 = ["cfg1", "cfg2-dropin", "cfg4-median", "cfg4-trimmed", "median256", "trimmed256", "cfg5", "delta", "inbox",
-          "digest-flow"]
-SUB_STEPS = {"cfg5": 2, "delta": 10, "inbox": 3, "digest-flow": 5}  # timed steps of the one-GPU sub-records
+          "digest-flow", "broadcast"]
+SUB_STEPS = {"cfg5": 2, "delta": 10, "inbox": 3, "digest-flow": 5, "broadcast": 5}  # timed steps of the one-GPU sub-records
 MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
 
@@ -973,8 +979,72 @@ def run_digest_flow(args, steps):
                                    "utils/crypto.py:56,95) over the same objects, same process"}}
 
 
+def run_broadcast_workload(args, seed, dev):
+    """Global-model serialization before the broadcast (SURVEY §8(f) row 4;
+    reference aggregator/aggregation.py:66-70): the tester pickles its
+    ResNet-18-sized state_dict into the 'global_model_update' envelope.  The
+    reference pickles the CUDA state_dict, so torch copies every tensor to
+    the host separately inside pickle.dumps; the product brings all fp32
+    tensors over in ONE transfer into a reused pinned buffer
+    (aggregation._host_state_dict) and pickles host views.  value = model
+    bytes serialized per second (device-to-host + pickle)."""
+    import pickle
+
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    shapes = resnet18_param_shapes()
+    model = torch.nn.Module()
+    for i, (nm, shape) in enumerate(shapes):
+        t = torch.empty(shape, dtype=torch.float32, device=dev)
+        ops.fill_synthetic_(t.view(-1), seed, i, W_SCALE)
+        model.register_parameter(nm.replace(".", "__"), torch.nn.Parameter(t, requires_grad=False))
+    torch.cuda.synchronize()
+
+    def envelope(state):
+        return pickle.dumps({"type": "global_model_update", "model": state, "addr": "127.0.0.1", "port": 1})
+
+    def ours():
+        return envelope(agg._host_state_dict(model.state_dict()))
+
+    def reference():
+        return envelope(model.state_dict())
+
+    if not args.no_check:
+        a, b = pickle.loads(ours())["model"], pickle.loads(reference())["model"]
+        ok = list(a) == list(b) and all(torch.equal(a[k], b[k].cpu()) for k in b)
+        log(f"broadcast: host state_dict envelope == the reference's: {ok}")
+        if not ok:
+            raise SystemExit("bench: broadcast payload differs from the reference's")
+
+    def timed(fn):
+        for _ in range(max(args.warmup, 1)):
+            fn()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        return (time.perf_counter() - t0) / args.steps
+
+    t_ours, t_ref = timed(ours), timed(reference)
+    nbytes = 4 * sum(_numel(s) for _, s in shapes)
+    del model
+    torch.cuda.empty_cache()
+    return {
+        "workload": "broadcast", "value": round(nbytes / t_ours / 1e9, 3), "unit": "GB/s", "steps": args.steps,
+        "ms_per_step": round(t_ours * 1e3, 3), "scaling": "weak", "dtype": "fp32",
+        "data": "synthetic ResNet-18-sized model on the GPU",
+        "config": {"workload": f"broadcast: the global_model_update envelope of a {len(shapes)}-tensor state_dict "
+                               f"({nbytes / 4:,.0f} params) pickled from the GPU model (SURVEY §8(f) row 4)",
+                   "reference_ms": round(t_ref * 1e3, 3), "speedup_vs_reference": round(t_ref / t_ours, 2),
+                   "parallelism": "single GPU, device-to-host"},
+        "roofline": {"bound": "pcie (device-to-host) + host pickle", "achieved": round(nbytes / t_ours / 1e9, 2),
+                     "peak": 63.0, "unit": "GB/s", "frac": round(nbytes / t_ours / 1e9 / 63.0, 4), "traffic": None},
+        "cpu_baseline": {"value": round(nbytes / t_ref / 1e9, 3), "unit": "GB/s", "kind": "reference", "cores": 1,
+                         "sample": "the reference's pickle.dumps of the CUDA state_dict envelope "
+                                   "(aggregation.py:70), same process"}}
+
+
 def replica_workload(args, name, dev):
-    """cfg5 / sha256 / delta / inbox (one GPU each): the workload's record."""
+    """cfg5 / sha256 / delta / inbox / broadcast (one GPU each): the workload's record."""
     rule, K, n, seed = WORKLOADS[name]
     if name == args.workload:
         K, n = args.peers or K, args.coords or n
@@ -984,6 +1054,8 @@ def replica_workload(args, name, dev):
         return run_digest_flow(args, args.steps)
     if rule == "delta":
         return run_delta_workload(args, n, seed, dev)
+    if rule == "broadcast":
+        return run_broadcast_workload(args, seed, dev)
     return run_inbox_workload(args, K, n, seed, dev)
 
 
@@ -1094,11 +1166,11 @@ def main():
     K = args.peers or K
     n = args.coords or n
     one_gpu = {"fused": "cfg5/sha256 run as replicas only", "sha256": "cfg5/sha256 run as replicas only",
-               "digest-flow": "digest-flow runs in one process",
+               "digest-flow": "digest-flow runs in one process", "broadcast": "broadcast runs on one GPU",
                "delta": "delta runs as replicas only", "inbox": "inbox runs on one GPU", "dropin": "drop-in runs on one GPU"}
     if rule in one_gpu and world > 1:
         raise SystemExit(one_gpu[rule] + " (one process per GPU)")
-    if rule in ("fused", "sha256", "delta", "inbox", "digest-flow"):
+    if rule in ("fused", "sha256", "delta", "inbox", "digest-flow", "broadcast"):
         rec = replica_workload(args, args.workload, dev)
         print(json.dumps({"metric": METRIC, "value": rec["value"], "unit": rec["unit"], "n_gpus": 1,
                           "steps": rec["steps"], "warmup": args.warmup, "ms_per_step": rec["ms_per_step"],
@@ -1133,7 +1205,7 @@ def main():
                     r, k2, n2, s2 = WORKLOADS[name]
                     if r == "dropin":
                         rec = measure_dropin(c, args, name, k2, s2, 30, 2, args.sub_cpu_seconds)
-                    elif r in ("fused", "delta", "inbox", "digest-flow"):
+                    elif r in ("fused", "delta", "inbox", "digest-flow", "broadcast"):
                         sargs = argparse.Namespace(**dict(vars(args), workload=name, steps=SUB_STEPS[name],
                                                           warmup=1, cpu_seconds=args.sub_cpu_seconds))
                         rec = replica_workload(sargs, name, dev)
