@@ -35,6 +35,9 @@ Sub-records (the "sub" object of the same line):
                 crypto.sign_data / verify_signature (vs 72 hashlib passes)
   broadcast     the global model's envelope pickled from the GPU (one D2H
                 transfer) vs the reference's pickle of the CUDA state_dict
+  cfg5_arrival  cfg5 as a node receives it: 256 x 100-MB messages in pinned
+                receive buffers landed with host SHA-256 beside the DMAs,
+                drop-in FedAvg over the accepted rows
 (N = 1 only, except cfg3_full, which runs at every N.)
 
 roofline.achieved = algorithmic bytes per launch 4n(K+2) / mean kernel time
@@ -88,6 +91,9 @@ WORKLOADS = {
     # land 16 serialized ResNet-18-sized updates (11.7M
     # params each) in the device slab vs the reference's pickle.loads
     "inbox": ("inbox", 16, 11_689_512, 0x5EED0007),
+    # cfg5 as a node receives it: messages in pinned host buffers, digests on
+    # the host beside the landing DMAs, FedAvg over the accepted slab rows
+    "cfg5-arrival": ("arrival", 256, 25_000_000, 0x5EED0004),
     # the global model pickled for the broadcast
     "broadcast": ("broadcast", 1, 11_689_512, 0x5EED0008),
     # the reference's per-round digest work: 72 sign/verify hashes over 3 MLP
@@ -95,8 +101,8 @@ WORKLOADS = {
     "digest-flow": ("digest-flow", 3, 535_818, 0),
 }
 SUB_N1 = ["cfg1", "cfg2-dropin", "cfg4-median", "cfg4-trimmed", "median256", "trimmed256", "cfg5", "delta", "inbox",
-          "digest-flow", "broadcast"]
-SUB_STEPS = {"cfg5": 2, "delta": 10, "inbox": 3, "digest-flow": 5, "broadcast": 5}  # timed steps of the one-GPU sub-records
+          "digest-flow", "broadcast", "cfg5-arrival"]
+SUB_STEPS = {"cfg5": 2, "delta": 10, "inbox": 3, "digest-flow": 5, "broadcast": 5, "cfg5-arrival": 2}  # timed steps of the one-GPU sub-records
 MSG_HEADER = 64  # bytes before the payload (keeps payloads 16-B aligned)
 
 
@@ -675,6 +681,121 @@ def run_digest_workload(args, rule, K, n, seed, dev):
     }
 
 
+def run_cfg5_arrival(args, K, n, seed, dev):
+    """cfg5 as a node receives it: K serialized updates ({'w': n fp32},
+    pickled like node/node.py:285) in the inbox's pinned receive buffers.
+    A step lands every message (one DMA + the landing kernel each) with its
+    SHA-256 on the host hashing threads beside the DMAs
+    (DeviceInbox.land(..., digest=True)), accepts the updates whose digest
+    matches what the sender signed, and runs the drop-in aggregate_models
+    (FedAvg) over the accepted slab rows.  The digest cache is emptied before
+    every step, so every message is hashed in every step.  value = hashed
+    bytes per second, as for cfg5."""
+    import hashlib
+    import pickle
+
+    import numpy as np
+
+    from p2pdl_amd.aggregator import aggregation as agg
+    from p2pdl_amd.node.inbox import DeviceInbox
+    from p2pdl_amd.utils import digests
+
+    from p2pdl_amd.node.inbox import ZeroCopyParser
+
+    proto = pickle.dumps({"w": torch.zeros(n)})
+    data = ZeroCopyParser(proto).parse()["w"].storage.data  # the payload's window of proto
+    pay = np.frombuffer(data, dtype=np.uint8).ctypes.data - np.frombuffer(proto, dtype=np.uint8).ctypes.data
+    assert len(data) == 4 * n and proto[pay:pay + 4 * n] == bytes(4 * n)
+    del data
+    nbytes = len(proto)
+    template = {"w": torch.empty(n, dtype=torch.float32, device=dev)}
+    inbox = DeviceInbox(template, k_max=K, device=dev, max_message_bytes=nbytes,
+                        pool_bytes=(K + 1) * nbytes)
+    log(f"cfg5-arrival: {K} pinned messages of {nbytes:,} B ({K * nbytes / 1e9:.1f} GB)")
+    stage = torch.empty(n, dtype=torch.float32, device=dev)
+    msgs, expected = [], []
+    for p in range(K):
+        m = inbox.message_buffer(nbytes)
+        m.buf[:pay].copy_(torch.frombuffer(bytearray(proto[:pay]), dtype=torch.uint8))
+        m.buf[pay + 4 * n:nbytes].copy_(torch.frombuffer(bytearray(proto[pay + 4 * n:]), dtype=torch.uint8))
+        ops.fill_synthetic_(stage, seed, p, UPD_SCALE)
+        m.buf[pay:pay + 4 * n].copy_(stage.view(torch.uint8))
+        msgs.append(m)
+    torch.cuda.synchronize()
+    pool = digests.hash_pool()
+    expected = list(pool.map(lambda m: hashlib.sha256(m.view()).digest(), msgs))  # what the senders signed
+    bad = [p for p in range(K) if (p * 7919) % 10 == 3]  # ~10% corrupted in flight, as cfg5
+    for p in bad:
+        msgs[p].buf[pay + 4000] ^= 0x40
+    w0 = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.fill_synthetic_(w0, seed, W_PEER, W_SCALE)
+    model = torch.nn.Module()
+    model.register_parameter("w", torch.nn.Parameter(w0.clone(), requires_grad=False))
+    node = types.SimpleNamespace(model=model, trainers_list=[], addr="127.0.0.1", port=1, neighbors=[],
+                                 received_models=[])
+    saved = agg.broadcast_global_model_update
+    agg.broadcast_global_model_update = lambda self: None
+
+    def step():
+        inbox.reset()
+        landed = [inbox.land(m, digest=True) for m in msgs]
+        ok = [inbox.digest(k) == expected[k] for k in range(K)]
+        node.received_models[:] = [{"model": u, "sender": k} for k, u in enumerate(landed) if ok[k]]
+        agg.aggregate_models(node)
+        torch.cuda.synchronize()
+        return ok
+
+    try:
+        times = []
+        for i in range(max(args.warmup, 1) + args.steps):
+            with torch.no_grad():
+                model.w.copy_(w0)
+            digests.CACHE.clear()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ok = step()
+            dt = time.perf_counter() - t0
+            if i >= max(args.warmup, 1):
+                times.append(dt)
+            if i == 0:
+                acc = [p for p in range(K) if ok[p]]
+                if acc != [p for p in range(K) if p not in bad]:
+                    raise SystemExit("bench: cfg5-arrival accepted the wrong updates")
+                if not args.no_check:
+                    import oracle  # checker only
+
+                    m_ = 4096
+                    want, _ = oracle.fedavg([oracle.synth(m_, seed, p, UPD_SCALE) for p in acc],
+                                            oracle.synth(m_, seed, W_PEER, W_SCALE))
+                    good = bits_equal(model.w[:m_].cpu().numpy(), want)
+                    log(f"cfg5-arrival: {len(acc)} accepted, FedAvg spot check vs oracle: "
+                        f"{'bit-exact' if good else 'MISMATCH'}")
+                    if not good:
+                        raise SystemExit("bench: cfg5-arrival FedAvg differs from the oracle")
+    finally:
+        agg.broadcast_global_model_update = saved
+        digests.CACHE.clear()
+    step_s = min(times)
+    hashed = K * nbytes
+    for m in msgs:
+        m.release()
+    del inbox, msgs, model, w0, stage, template, node
+    import gc
+
+    gc.collect()  # the inbox and its pinned buffers refer to each other
+    torch.cuda.empty_cache()
+    return {
+        "workload": "cfg5_arrival", "value": round(hashed / step_s / 1e9, 3), "unit": "GB/s", "steps": args.steps,
+        "ms_per_step": round(step_s * 1e3, 3), "scaling": "weak", "dtype": "u32 (SHA-256) + fp32",
+        "data": "synthetic serialized updates (pickled {'w': 25M fp32}, device-PRNG payload) in pinned memory",
+        "config": {"workload": f"cfg5 at arrival: {K} messages x {nbytes:,} B landed from the inbox's pinned "
+                               f"buffers with host SHA-256 beside the DMAs, {len(bad)} corrupted, drop-in FedAvg "
+                               f"over the {K - len(bad)} accepted", "parallelism": "single GPU, host hashing"},
+        "roofline": {"bound": "host SHA-NI threads / PCIe", "achieved": round(hashed / step_s / 1e9, 2),
+                     "peak": 63.0, "unit": "GB/s", "frac": round(hashed / step_s / 1e9 / 63.0, 4), "traffic": None},
+        "cpu_baseline": None}
+
+
 # ------------------------------------------------------------------ delta / inbox
 def run_delta_workload(args, n, seed, dev):
     """Trainer-side local update (reference node/node.py:273-282) of one
@@ -1056,6 +1177,8 @@ def replica_workload(args, name, dev):
         return run_delta_workload(args, n, seed, dev)
     if rule == "broadcast":
         return run_broadcast_workload(args, seed, dev)
+    if rule == "arrival":
+        return run_cfg5_arrival(args, K, n, seed, dev)
     return run_inbox_workload(args, K, n, seed, dev)
 
 
@@ -1167,10 +1290,11 @@ def main():
     n = args.coords or n
     one_gpu = {"fused": "cfg5/sha256 run as replicas only", "sha256": "cfg5/sha256 run as replicas only",
                "digest-flow": "digest-flow runs in one process", "broadcast": "broadcast runs on one GPU",
+               "arrival": "cfg5-arrival runs as replicas only",
                "delta": "delta runs as replicas only", "inbox": "inbox runs on one GPU", "dropin": "drop-in runs on one GPU"}
     if rule in one_gpu and world > 1:
         raise SystemExit(one_gpu[rule] + " (one process per GPU)")
-    if rule in ("fused", "sha256", "delta", "inbox", "digest-flow", "broadcast"):
+    if rule in ("fused", "sha256", "delta", "inbox", "digest-flow", "broadcast", "arrival"):
         rec = replica_workload(args, args.workload, dev)
         print(json.dumps({"metric": METRIC, "value": rec["value"], "unit": rec["unit"], "n_gpus": 1,
                           "steps": rec["steps"], "warmup": args.warmup, "ms_per_step": rec["ms_per_step"],
@@ -1205,7 +1329,7 @@ def main():
                     r, k2, n2, s2 = WORKLOADS[name]
                     if r == "dropin":
                         rec = measure_dropin(c, args, name, k2, s2, 30, 2, args.sub_cpu_seconds)
-                    elif r in ("fused", "delta", "inbox", "digest-flow", "broadcast"):
+                    elif r in ("fused", "delta", "inbox", "digest-flow", "broadcast", "arrival"):
                         sargs = argparse.Namespace(**dict(vars(args), workload=name, steps=SUB_STEPS[name],
                                                           warmup=1, cpu_seconds=args.sub_cpu_seconds))
                         rec = replica_workload(sargs, name, dev)
