@@ -220,10 +220,20 @@ def _slab_fast_path(st, keys, ws, received, rule, lr, trim_frac) -> bool:
         if st is not None:
             st.extra["slab"] = (weakref.ref(inbox), offsets)
     inbox.order_after_landing()  # land()'s row copies ran on the listener thread's stream
-    rows = [rm["model"].row for rm in received]
-    ops.aggregate_slab_rows_(ws, inbox.slab, rows, offsets, rule, lr=lr, trim_frac=trim_frac,
-                             w_ptrs=st.ptrs if st is not None else None,
-                             numels=st.numels if st is not None else None)
+    rows = tuple(rm["model"].row for rm in received)
+    # the launch itself is cached on the validated model-state entry: the same
+    # rows, rule and trim as the last call over this inbox -> the same device
+    # table, launched again with no per-call work (ops.relaunch)
+    ck = (rows, rule, trim_frac)
+    last = st.extra.get("launch") if st is not None else None
+    if last is not None and last[0] == ck and last[1]() is inbox:
+        ops.relaunch(last[2], inbox.slab.device, len(ws), len(rows), lr)
+    else:
+        entry = ops.aggregate_slab_rows_(ws, inbox.slab, rows, offsets, rule, lr=lr, trim_frac=trim_frac,
+                                         w_ptrs=st.ptrs if st is not None else None,
+                                         numels=st.numels if st is not None else None)
+        if st is not None and entry is not None:
+            st.extra["launch"] = (ck, weakref.ref(inbox), entry)
     inbox.slab_consumed()  # the next round's land() into these rows waits for this kernel
     return True
 

@@ -245,10 +245,13 @@ def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_fra
     with torch.cuda.device(dev):
         _launch_table(base, L, tiles, K, r, b, lr)
     if cache_key is not None:
+        entry = (buf, tiles, r, b, torch.cuda.current_stream(dev).cuda_stream)
         with _TABLES_LOCK:
-            _TABLES[cache_key] = (buf, tiles, r, b, torch.cuda.current_stream(dev).cuda_stream)
+            _TABLES[cache_key] = entry
             while len(_TABLES) > _TABLES_MAX:
                 _TABLES.popitem(last=False)
+        return entry
+    return None
 
 
 def aggregate_segments_(ws: Sequence[torch.Tensor], peer_lists: Sequence[Sequence[torch.Tensor]],
@@ -337,7 +340,7 @@ def aggregate_ptr_table_(ws: Sequence[torch.Tensor], ptrs: np.ndarray, rule="fed
 def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: Sequence[int],
                          offsets: Sequence[int], rule="fedavg", *, lr: float = 0.1,
                          trim_b: int | None = None, trim_frac: float = DEFAULT_TRIM_FRAC,
-                         w_ptrs: tuple | None = None, numels: tuple | None = None) -> None:
+                         w_ptrs: tuple | None = None, numels: tuple | None = None):
     """aggregate_segments_ for updates that are rows of one [K_max, N] fp32
     slab (what node.inbox.DeviceInbox lands): update j's tensor for key l is
     slab[rows[j], offsets[l] : offsets[l] + ws[l].numel()].  The (L, K) peer
@@ -345,7 +348,9 @@ def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: S
     ``w_ptrs``: the ws' data pointers, from a caller that has already checked
     ws (fp32, contiguous, on the slab's device) and vouches they are
     unchanged (aggregation.py's validated model-state cache); the per-tensor
-    checks are then skipped (``numels``: their element counts, likewise)."""
+    checks are then skipped (``numels``: their element counts, likewise).
+    Returns the device-table cache entry it launched (``relaunch`` takes
+    it), or None when there was nothing to launch."""
     L, K = len(ws), len(rows)
     if L == 0:
         return
@@ -368,13 +373,8 @@ def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: S
         if hit is not None:
             _TABLES.move_to_end(key)
     if hit is not None:  # same addresses and sizes as a previous call: same table
-        buf, tiles, r, b, alloc_stream = hit
-        with torch.cuda.device(dev) if torch.cuda.current_device() != dev.index else _NO_CTX:
-            raw = N.stream_handle(dev)
-            if raw != alloc_stream:
-                buf.record_stream(torch.cuda.current_stream(dev))  # eviction must not recycle it under this launch
-            _launch_table(buf.data_ptr(), L, tiles, K, r, b, lr, stream=raw)
-        return
+        relaunch(hit, dev, L, K, lr)
+        return hit
     rows_a = np.asarray(rows, dtype=np.int64)
     offs_a = np.asarray(offsets, dtype=np.int64)
     kmax, width = slab.shape
@@ -385,7 +385,21 @@ def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: S
     base, stride = slab.data_ptr(), width * 4
     ptrs = (np.uint64(base) + rows_a.astype(np.uint64)[None, :] * np.uint64(stride)
             + offs_a.astype(np.uint64)[:, None] * np.uint64(4))
-    _launch_segments(ws, ptrs, numels, rule, K, lr, trim_b, trim_frac, None, dev, cache_key=key)
+    return _launch_segments(ws, ptrs, numels, rule, K, lr, trim_b, trim_frac, None, dev, cache_key=key)
+
+
+def relaunch(entry, dev, L: int, K: int, lr: float) -> None:
+    """Launch a cached device segment table again (an entry that
+    aggregate_slab_rows_ / aggregate_ptr_table_ returned): the same kernel
+    over the same addresses, on the current stream of ``dev`` -- no table
+    work, no H2D copy, no per-call checks (the caller vouches that the
+    addresses it was built from are unchanged)."""
+    buf, tiles, r, b, alloc_stream = entry
+    with torch.cuda.device(dev) if torch.cuda.current_device() != dev.index else _NO_CTX:
+        raw = N.stream_handle(dev.index)
+        if raw != alloc_stream:
+            buf.record_stream(torch.cuda.current_stream(dev))  # eviction must not recycle it under this launch
+        _launch_table(buf.data_ptr(), L, tiles, K, r, b, lr, stream=raw)
 
 
 # ------------------------------------------------------------------ K4

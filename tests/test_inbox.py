@@ -601,6 +601,42 @@ def test_slab_table_cache_across_rounds_and_streams(cuda, monkeypatch):
     mine = [key for key in ops._TABLES if key[1:3] == (inbox.slab.data_ptr(), k + 1)]
     assert len(mine) == 2  # one table per row set (0..3, 1..4), reused across rounds and streams
 
+    # the launch cache on the model-state entry: same rows + rule -> relaunch
+    # (no aggregate_slab_rows_ call); a rule change on the same rows -> a new
+    # table, not the FedAvg one launched again
+    calls = {"relaunch": 0, "table": 0}
+    real_relaunch, real_rows = ops.relaunch, ops.aggregate_slab_rows_
+
+    def counted(name, fn):
+        def f(*a, **kw):
+            calls[name] += 1
+            return fn(*a, **kw)
+        return f
+
+    monkeypatch.setattr(ops, "relaunch", counted("relaunch", real_relaunch))
+    monkeypatch.setattr(ops, "aggregate_slab_rows_", counted("table", real_rows))
+    for rnd, rule in enumerate(["fedavg", "fedavg", "median", "median", "trimmed", "fedavg"]):
+        inbox.reset()
+        ser = [pickle.dumps(mlp_update(300 + 10 * rnd + j)) for j in range(k)]
+        landed = [inbox.land(s_, r) for s_, r in zip(ser, range(k))]
+        node.received_models = [{"model": u, "sender": j} for j, u in enumerate(landed)]
+        flat = [np.concatenate([pickle.loads(s)[name].numpy().reshape(-1) for name, _ in MLP_SHAPES])
+                for s in ser]
+        if rule == "fedavg":
+            want, _ = oracle.fedavg(flat, w)
+        else:
+            r = ops.rule_id(rule)
+            want, _ = oracle.robust(flat, r, ops.trim_count(k) if r == 2 else 0, w=w)
+        agg.aggregate_models(node, rule=rule)
+        got = np.concatenate([t.detach().cpu().numpy().reshape(-1) for t in model.state_dict().values()])
+        assert_bits_equal(got, want, what=f"launch-cache round {rnd} {rule}")
+        w = want
+    # fedavg (the launch cached by the last round above), fedavg, median (new
+    # table), median, trimmed (new table), fedavg (launch cache holds trimmed:
+    # aggregate_slab_rows_, which finds the FedAvg table in _TABLES and
+    # relaunches it)
+    assert calls == {"relaunch": 4, "table": 3}
+
 
 # ---- K5 device path: the message in pinned memory, one DMA, the landing kernel
 def _pinned(inbox, data):
