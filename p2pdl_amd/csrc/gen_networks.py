@@ -28,17 +28,27 @@ themselves be computed); an exact MILP of the same selection problem finds
 at most 0.7% more.  sort128: 2942 -> 2184 VALU (round 2's 16-block network:
 2894), bmerge128 pruned to ranks 51..127: 619 -> 430.
 
+Three-list merges (round 4, MSort below): the sorts are trees of merges of
+THREE sorted lists whose cleanup is one three-input operation per output --
+sort128 1962 instead of 2120 (Batcher lowered), sort64 731 / 789, median128
+1370 / 1658, trim128 1786 / 1976; the pruned parity mergers of the K = 256
+trimmed mean split by index modulo 3 (390 / 398).
+
 Output: networks.inc (committed; regenerate with `python gen_networks.py`;
 `--classic` writes the round-2 two-input form, for A/B builds only).
 Each network is emitted as a device function  net_<tag><ASC>(T (&v)[KP], hook).
 
-Verification: `python gen_networks.py --check` runs every emitted program
+Verification: every MSort stage asserts each output against its rank on the
+stage's whole 0-1 domain as it is built (a proof by the 0-1 principle: min,
+max and med3 commute with thresholds).  `python gen_networks.py --check`
+runs every emitted program
 (the instruction list as emitted, three-input ops included) on 0-1 inputs --
 exhaustively for KP <= 16, on every domain vector of a bitonic merger -- and
 on random 32-bit inputs, against sorted().
 """
 from __future__ import annotations
 
+import itertools
 import os
 import random
 import sys
@@ -122,6 +132,150 @@ def batcher_stages(n: int, lo: int = 0):
             + [(c, ("merge", lo, n)) for c in oddeven_merge(lo, lo + n - 1, 1)])
 
 
+# ---- Three-list merge sort ("msort", round 4) --------------------------------
+# Batcher's merge splits two sorted lists by index parity, merges the classes
+# and fixes the interleaving with one layer of comparators.  The same scheme
+# works for THREE sorted lists: split each by parity, merge the three even
+# classes and the three odd classes (recursively), interleave, and every
+# output of the merge is then ONE min / max / min3 / max3 / med3 of the
+# interleaved values in a window of +-6 around its rank (found by search and
+# proved on the stage's 0-1 domain: all combinations of the lists' zero
+# counts).  Four lists do not close with one operation per output.  A sort
+# tree of three-list merges (MSORT_TREE, from `--search`: the lowered
+# instruction count of every candidate split) sorts 128 keys in 1962
+# instructions against 2120 for the lowered Batcher sort, 64 in 731 / 789.
+# Every stage is built as SSA nodes with their values on that stage's domain,
+# so Program's three-input absorption applies unchanged.
+MSORT_TREE = {128: (43, 43, 42), 64: (22, 21, 21), 43: (15, 14, 14), 42: (14, 14, 14), 32: (12, 10, 10),
+              22: (8, 7, 7), 21: (9, 6, 6), 16: (9, 7), 15: (9, 6), 14: (9, 5), 12: (4, 4, 4), 10: (4, 3, 3),
+              9: (3, 3, 3), 8: (3, 3, 2), 7: (4, 3), 6: (3, 3), 5: (3, 2)}
+MSORT_WINDOW = 6
+
+
+def _pack(mask) -> int:
+    """A numpy bool vector as an int bitset (bit s = element s)."""
+    import numpy as np
+
+    return int.from_bytes(np.packbits(mask, bitorder="little").tobytes(), "little")
+
+
+class MSort:
+    """SSA nodes of a three-list merge sort: kind / args / stage per node as in
+    Program; bits[stage][node] = the node's values on the stage's 0-1 domain."""
+
+    def __init__(self, kp: int):
+        self.kp = kp
+        self.kind = ["in"] * kp
+        self.args = [()] * kp
+        self.stage = [None] * kp
+        self.bits = {}
+
+    def _op(self, st, kind, args, cache):
+        key = (kind, tuple(sorted(args)))
+        if key in cache:
+            return cache[key]
+        b = self.bits[st]
+        xs = [b[a] for a in key[1]]
+        if kind in ("lo", "lo3"):
+            m = xs[0] & xs[1] & (xs[2] if len(xs) > 2 else -1)
+        elif kind in ("hi", "hi3"):
+            m = xs[0] | xs[1] | (xs[2] if len(xs) > 2 else 0)
+        else:  # med3 = majority
+            m = (xs[0] & xs[1]) | (xs[0] & xs[2]) | (xs[1] & xs[2])
+        self.kind.append(kind)
+        self.args.append(key[1])
+        self.stage.append(st)
+        i = len(self.kind) - 1
+        b[i] = m
+        cache[key] = i
+        return i
+
+    def sort(self, wires, tree=None):
+        tree = MSORT_TREE if tree is None else tree
+        n = len(wires)
+        if n <= 4:
+            return self.merge([[w] for w in wires])
+        lists, i = [], 0
+        for part in tree[n]:
+            lists.append(self.sort(wires[i:i + part], tree))
+            i += part
+        return self.merge(lists)
+
+    def merge(self, lists, k=2, win=MSORT_WINDOW):
+        """One stage: merge 2-4 sorted node lists (4 only of single nodes),
+        splitting by index modulo k (an int, or a function of the longest
+        list's length).  Returns the output nodes, each checked against its
+        rank on the whole 0-1 domain of the stage."""
+        import numpy as np
+
+        st = ("mmerge", len(self.bits))
+        sizes = [len(x) for x in lists]
+        zs = [g.reshape(-1) for g in np.meshgrid(*[np.arange(s + 1) for s in sizes], indexing="ij")]
+        b = self.bits[st] = {}
+        for z, lst in zip(zs, lists):
+            for j, x in enumerate(lst):
+                b[x] = _pack(z <= j)  # a sorted 0-1 list with z zeros: element j is 1 iff j >= z
+        out = self._merge(st, list(lists), zs, k, win, {})
+        total = sum(zs)
+        assert all(b[x] == _pack(total <= t) for t, x in enumerate(out)), (st, sizes)
+        return out
+
+    def _merge(self, st, lists, zs, k, win, cache):
+        import numpy as np
+
+        pairs = [(lst, z) for lst, z in zip(lists, zs) if lst]
+        lists, zs = [p[0] for p in pairs], [p[1] for p in pairs]
+        op = lambda kind, *a: self._op(st, kind, a, cache)  # noqa: E731
+        if len(lists) == 1:
+            return list(lists[0])
+        if all(len(x) == 1 for x in lists):
+            v = [x[0] for x in lists]
+            if len(v) == 2:
+                return [op("lo", *v), op("hi", *v)]
+            if len(v) == 3:
+                return [op("lo3", *v), op("med3", *v), op("hi3", *v)]
+            a, b_, c, d = v  # sort3, then d inserted by med3 (7 instructions)
+            t0, t1, t2 = op("lo3", a, b_, c), op("med3", a, b_, c), op("hi3", a, b_, c)
+            return [op("lo", t0, d), op("med3", t0, t1, d), op("med3", t1, t2, d), op("hi", t2, d)]
+        if len(lists) == 2 and min(len(x) for x in lists) == 1:  # insertion: n + 1 (optimal)
+            big, one = (lists[0], lists[1][0]) if len(lists[1]) == 1 else (lists[1], lists[0][0])
+            return ([op("lo", big[0], one)] + [op("med3", big[i - 1], big[i], one) for i in range(1, len(big))]
+                    + [op("hi", big[-1], one)])
+        assert len(lists) <= 3, "four lists do not close with one operation per output"
+        longest = max(len(x) for x in lists)
+        kk = min(k(longest) if callable(k) else k, longest)
+        subs = []
+        for r in range(kk):  # class r of every list: its zero count is ceil((z - r) / kk)
+            subs.append(self._merge(st, [x[r::kk] for x in lists],
+                                    [np.maximum(0, (z - r + kk - 1) // kk) for z in zs], k, win, cache))
+        seq = [subs[r][i] for i in range(max(map(len, subs))) for r in range(kk) if i < len(subs[r])]
+        total = sum(zs)
+        b = self.bits[st]
+        out = []
+        for t in range(len(seq)):
+            want = _pack(total <= t)
+            pos = range(max(0, t - win), min(len(seq), t + win + 1))
+            f = next((seq[i] for i in pos if b[seq[i]] == want), None)
+            if f is None:
+                for i, j in itertools.combinations(pos, 2):
+                    x, y = b[seq[i]], b[seq[j]]
+                    if x & y == want or x | y == want:
+                        f = op("lo" if x & y == want else "hi", seq[i], seq[j])
+                        break
+            if f is None:
+                for i, j, l in itertools.combinations(pos, 3):
+                    x, y, z = b[seq[i]], b[seq[j]], b[seq[l]]
+                    kind = ("lo3" if x & y & z == want else "hi3" if x | y | z == want
+                            else "med3" if (x & y) | (x & z) | (y & z) == want else None)
+                    if kind:
+                        f = op(kind, seq[i], seq[j], seq[l])
+                        break
+            if f is None:
+                raise ValueError(f"no one-operation output for rank {t} of a merge of {[len(x) for x in lists]}")
+            out.append(f)
+        return out
+
+
 def bitonic_merge(n: int):
     """Comparators sorting a BITONIC sequence of n (power of 2) ascending:
     half-cleaners at distance n/2, n/4, ..., 1."""
@@ -143,7 +297,7 @@ def merge_stage(n: int):
 
 
 NETWORKS = {"bmerge": bitonic_merge, "sort": batcher_stages, "merge": merge_stage}
-CLASSIC = {"bmerge": bitonic_merge, "sort": green_batcher, "merge": merge_stage}
+CLASSIC = {"bmerge": bitonic_merge, "sort": green_batcher, "msort": green_batcher, "merge": merge_stage}
 
 
 def domain(stage):
@@ -402,6 +556,92 @@ class Program:
         return res
 
 
+class MSortProgram(Program):
+    """Program over an MSort network, pruned to the wanted ranks by liveness."""
+
+    def __init__(self, kp, wanted, tree=None, net=None):
+        if net is None:
+            net = MSort(kp)
+            outs = net.sort(list(range(kp)), tree)
+        else:
+            net, outs = net
+        self.kp = kp
+        self.kind, self.args, self.stage, self.bits = net.kind, net.args, net.stage, net.bits
+        self.out = {w: outs[w] for w in wanted}
+        live = set(self.out.values())
+        for i in range(len(self.kind) - 1, -1, -1):
+            if i in live:
+                live.update(self.args[i])
+        self.live = live
+        self.absorbed = {}
+        self.elim = set()
+        self._ins = None
+
+
+def merge_cost(sizes, k=2) -> int:
+    """Lowered instruction count of one merge stage of sorted lists of `sizes`."""
+    n = sum(sizes)
+    net = MSort(n)
+    lists, i = [], 0
+    for s in sizes:
+        lists.append(list(range(i, i + s)))
+        i += s
+    outs = net.merge(lists, k)
+    return min(len(MSortProgram(n, range(n), net=(net, outs)).fuse(reverse=r).instrs()) for r in (True, False))
+
+
+def search_tree(sizes=(128, 64, 32, 16, 8), spread=2, wide_below=0, wide=6):
+    """The MSORT_TREE search: for each n the cheapest split into two or three
+    near-balanced parts (each part up to `spread` above the balanced size;
+    `wide` for n <= wide_below), scored by lowered instruction counts."""
+    import functools
+
+    @functools.lru_cache(None)
+    def mc(parts):
+        try:
+            return merge_cost(parts)
+        except (ValueError, AssertionError):
+            return None
+
+    @functools.lru_cache(None)
+    def best(n):
+        if n <= 4:
+            return ({1: 0, 2: 2, 3: 3, 4: 7}[n], None)
+        cands = []
+        sp = wide if n <= wide_below else spread
+        for a in range((n + 1) // 2, min(n - 1, (n + 1) // 2 + sp) + 1):
+            cands.append((a, n - a))
+        for a in range(-(-n // 3), -(-n // 3) + sp + 1):
+            for b2 in range(-(-(n - a) // 2), -(-(n - a) // 2) + sp):
+                c = n - a - b2
+                if 1 <= c <= b2 <= a:
+                    cands.append((a, b2, c))
+        top = None
+        for parts in cands:
+            m = mc(parts)
+            if m is None:
+                continue
+            tot = m + sum(best(x)[0] for x in parts)
+            if top is None or tot < top[0]:
+                top = (tot, parts)
+        return top
+
+    for n in sizes:
+        print(n, best(n), flush=True)
+    tree = {}
+
+    def walk(n):
+        parts = best(n)[1]
+        if parts:
+            tree[n] = parts
+            for x in parts:
+                walk(x)
+
+    for n in sizes:
+        walk(n)
+    print("MSORT_TREE =", dict(sorted(tree.items(), reverse=True)))
+
+
 def network_specs():
     """(tag, KP, wanted ranks or None = full sort, base network).
 
@@ -411,14 +651,14 @@ def network_specs():
     (robust_lds.hip, either direction, bmerge64 across lanes)."""
     specs = []
     for kp in (2, 4, 8, 16, 32, 64, 128):
-        specs.append((f"sort{kp}", kp, None, "sort"))
+        specs.append((f"sort{kp}", kp, None, "msort"))
     for kp in (32, 64, 128):
         specs.append((f"bmerge{kp}", kp, None, "bmerge"))
     # specialised K == KP instances for the benchmark configurations
     for kp in (64, 128):
-        specs.append((f"median{kp}", kp, [(kp - 1) // 2], "sort"))
+        specs.append((f"median{kp}", kp, [(kp - 1) // 2], "msort"))
         b = int(0.2 * kp + 1e-9)
-        specs.append((f"trim{kp}_b{b}", kp, list(range(b, kp - b)), "sort"))
+        specs.append((f"trim{kp}_b{b}", kp, list(range(b, kp - b)), "msort"))
     # trimmed mean of 256 (robust_pair.hip): Batcher's odd-even merge of the
     # two waves' sorted 128 split by parity -- v = merge(A_even, B_even) in
     # wave 0, w = merge(A_odd, B_odd) in wave 1; ranks 51..204 of the merge
@@ -429,9 +669,33 @@ def network_specs():
     return specs
 
 
+_MSORT_NETS = {}
+
+
 def build(tag, kp, wanted, base):
-    ops = prune(NETWORKS[base](kp), wanted if wanted is not None else range(kp))
+    """(comparator list or None, lowered Program).  "msort": the three-list
+    merge sort, or Batcher's lowered sort where that is shorter (pruned specs
+    can go either way) -- the returned base says which."""
     want = list(range(kp)) if wanted is None else wanted
+    if base == "merge":  # Batcher's merge, or the residue-3 split above 4 keys per list if shorter
+        net = MSort(kp)
+        outs = net.merge([list(range(kp // 2)), list(range(kp // 2, kp))], k=lambda n: 3 if n > 4 else 2)
+        best = min((MSortProgram(kp, want, net=(net, outs)).fuse(reverse=r) for r in (True, False)),
+                   key=lambda p: len(p.instrs()))
+        ops = prune(NETWORKS[base](kp), want)
+        other = min((Program(ops, kp, want).fuse(reverse=r) for r in (True, False)), key=lambda p: len(p.instrs()))
+        return (ops, other) if len(other.instrs()) <= len(best.instrs()) else (None, best)
+    if base == "msort":
+        if kp not in _MSORT_NETS:
+            net = MSort(kp)
+            _MSORT_NETS[kp] = (net, net.sort(list(range(kp))))
+        best = min((MSortProgram(kp, want, net=_MSORT_NETS[kp]).fuse(reverse=r) for r in (True, False)),
+                   key=lambda p: len(p.instrs()))
+        ops, other = build(tag, kp, wanted, "sort")
+        if len(other.instrs()) < len(best.instrs()):
+            return ops, other
+        return None, best
+    ops = prune(NETWORKS[base](kp), wanted if wanted is not None else range(kp))
     # the better of a backward and a forward greedy pass
     best = min((Program(ops, kp, want).fuse(reverse=r) for r in (True, False)), key=lambda p: len(p.instrs()))
     return ops, best
@@ -473,10 +737,15 @@ def emit_fused():
     for tag, kp, wanted, base in network_specs():
         ops, prog = build(tag, kp, wanted, base)
         ins = prog.instrs()
-        nce = sum(1 for o, _ in ops if o[0] == "CE") + 5 * sum(1 for o, _ in ops if o[0] == "SORT4")
         cnt = {k: sum(1 for _, op, _ in ins if op == k) for k in ("lo3", "hi3", "med3")}
-        lines.append(f"// {tag}: KP={kp} wanted={'all' if wanted is None else f'{wanted[0]}..{wanted[-1]}'}"
-                     f" comparators={nce} two-input valu={2 * nce + sum(1 for o, _ in ops if o[0] in ('MIN', 'MAX'))} -> {len(ins)}"
+        rng = 'all' if wanted is None else f'{wanted[0]}..{wanted[-1]}'
+        if ops is None:
+            shape = "three-list merge sort" if base == "msort" else "residue-3 merge"
+        else:
+            nce = sum(1 for o, _ in ops if o[0] == "CE") + 5 * sum(1 for o, _ in ops if o[0] == "SORT4")
+            shape = (f"comparators={nce} two-input valu="
+                     f"{2 * nce + sum(1 for o, _ in ops if o[0] in ('MIN', 'MAX'))} ->")
+        lines.append(f"// {tag}: KP={kp} wanted={rng} {shape} {len(ins)}"
                      f" (min3 {cnt['lo3']}, max3 {cnt['hi3']}, med3 {cnt['med3']})")
         lines.append("template <bool ASC, typename T, typename H = NoHook>  // ASC=false sorts descending")
         lines.append(f"__device__ __forceinline__ void net_{tag}(T (&v)[{kp}], H&& hook = H{{}}) {{")
@@ -489,7 +758,7 @@ def emit_fused():
             # hook(v, blk) runs before the first instruction that reads input
             # block blk (16 keys) -- v still holds the inputs there
             blks = {x // 16 for x in a if x is not None and x < kp}
-            for blk in sorted(blks - seen) if kp >= 16 and base == "sort" else ():
+            for blk in sorted(blks - seen) if kp >= 16 and base in ("sort", "msort") else ():
                 lines.append(f"  hook(v, {blk});")
                 seen.add(blk)
             if op == "lo":
@@ -539,15 +808,18 @@ def check():
         ref = np.sort(inputs, axis=1)[:, want]
         fused = prog.run(inputs)[:, want]
         assert np.array_equal(fused, ref), (tag, "fused")
-        for vals in inputs[:: max(1, len(inputs) // 300)].tolist():  # the classic form, spot-checked
-            got, srt = apply(ops, vals), sorted(vals)
+        for vals in inputs[:: max(1, len(inputs) // 300)].tolist() if ops is not None else ():
+            got, srt = apply(ops, vals), sorted(vals)  # the classic form, spot-checked
             assert all(got[r] == srt[r] for r in want), (tag, "classic", vals)
-        print(f"{tag}: ok ({len(ops)} comparators, {len(prog.instrs())} instructions, {len(inputs)} inputs)")
+        form = f"{len(ops)} comparators" if ops is not None else f"SSA {base}"
+        print(f"{tag}: ok ({form}, {len(prog.instrs())} instructions, {len(inputs)} inputs)")
 
 
 if __name__ == "__main__":
     if "--check" in sys.argv:
         check()
+    elif "--search" in sys.argv:
+        search_tree()
     else:
         lines = emit_classic() if "--classic" in sys.argv else emit_fused()
         with open(os.path.join(HERE, "networks.inc"), "w") as f:
