@@ -100,6 +100,35 @@ def test_committed_networks_are_the_generated_ones():
         assert f.read() == "\n".join(gen_networks.emit_fused())
 
 
+def test_three_list_merges_close_with_one_operation_per_output():
+    """The three-list merge (gen_networks.MSort): every output of a merge of
+    three sorted lists is one min / max / min3 / max3 / med3, proved on the
+    stage's 0-1 domain as it is built and re-checked here on random sorted
+    lists of integers with ties; four lists do not close that way."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "p2pdl_amd", "csrc"))
+    import gen_networks as G
+
+    rng = np.random.default_rng(3)
+    for sizes in [(3, 3, 2), (8, 8, 8), (9, 6, 6), (15, 14, 14)]:
+        n = sum(sizes)
+        net = G.MSort(n)
+        lists, i = [], 0
+        for s in sizes:
+            lists.append(list(range(i, i + s)))
+            i += s
+        outs = net.merge(lists)
+        prog = G.MSortProgram(n, range(n), net=(net, outs)).fuse()
+        x = rng.integers(0, 5, size=(500, n)).astype(np.uint64)
+        i = 0
+        for s in sizes:
+            x[:, i:i + s] = np.sort(x[:, i:i + s], axis=1)
+            i += s
+        assert np.array_equal(prog.run(x), np.sort(x, axis=1)), sizes
+    assert G.merge_cost((8, 8, 8)) == 82  # two lowered Batcher merges: 37 + 60
+    with pytest.raises(AssertionError):
+        G.MSort(16).merge([[0, 1, 2, 3], [4, 5, 6, 7], [8, 9, 10, 11], [12, 13, 14, 15]])
+
+
 def test_delta_snapshot_oracle_matches_torch_reference_ops():
     """oracle.delta_snapshot_np == the reference's torch ops (node/node.py:275,279,282)."""
     import torch
