@@ -76,6 +76,12 @@ WORKLOADS = {
     # north-star robust target: median over 256 peers (cfg3's K) on a 100M tile
     "median256": ("median", 256, 100_000_000, 0x5EED0005),
     "trimmed256": ("trimmed", 256, 100_000_000, 0x5EED0005),
+    # K between the kernel families' sizes: the 4-lanes-per-coordinate LDS
+    # kernels (K 129..255); not a BASELINE config, run on request only
+    "median200": ("median", 200, 100_000_000, 0x5EED0009),
+    "trimmed200": ("trimmed", 200, 100_000_000, 0x5EED0009),
+    "median96": ("median", 96, 100_000_000, 0x5EED000A),
+    "trimmed96": ("trimmed", 96, 100_000_000, 0x5EED000A),
     # cfg5: 256 serialized updates (64-B header + 25M fp32 payload), digest all,
     # reject the ~10% whose bytes were corrupted, FedAvg the accepted ones
     "cfg5": ("fused", 256, 25_000_000, 0x5EED0004),

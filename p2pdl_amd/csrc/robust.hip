@@ -26,41 +26,66 @@ namespace p2p {
 
 constexpr int kRobustTile = 128;  // coordinates per block (one lane each)
 
+// PAD (round 4): K in KP/2+1..KP-1 (or another trim) runs the K == KP
+// networks on KP slots, slots >= K being pads -- the first `lo` of them the
+// bottom of the order (-inf / key 0), the rest the top (+inf / key ~0); every
+// real key orders between them and ties are the same value.  Median:
+// lo = (KP-1)/2 - (K-1)/2 puts the real lower median at rank (KP-1)/2, the
+// four-list search's.  Trimmed: lo = b0 - b (b0 = floor(0.2 KP), the pruned
+// network's) puts the kept real ranks b..K-b-1 at b0..b0+m-1 (m = K - 2b),
+// summed while k < m.  robust_pad_fits says when the pads fit.  A pad slot
+// loads from a pad row (robust_nets.h pad_row), so the networks and the NaN
+// test see the pads with no select.
+__host__ __device__ constexpr int pad_lo(int KP, int rule, int K, int trim_b) {
+  return rule == P2P_RULE_MEDIAN ? (KP - 1) / 2 - (K - 1) / 2 : (KP * 2) / 10 - trim_b;
+}
+
 // K == KP: the pruned rules on the float values (robust_nets.h: same ranks and
 // bits as the keys) -- no key map in (2 VALU per key) or out.  `nan` collects
 // the NaN test block by block as the networks first read each block; the
 // result is valid only when it stays 0.
-template <int KP, int RULE>
-__device__ __forceinline__ float special_floats(const uint32_t (&v)[KP], uint64_t& nan) {
+template <int KP, int RULE, bool PAD = false>
+__device__ __forceinline__ float special_floats(const uint32_t (&v)[KP], uint64_t& nan, int K = KP, int trim_b = 0) {
+  auto at = [&](int j) { return __uint_as_float(v[j]); };
   if constexpr (RULE == P2P_RULE_MEDIAN) {
     constexpr int Q = KP / 4;
     fk a[Q], b[Q], c[Q], d[Q];
 #pragma unroll
     for (int j = 0; j < Q; ++j) {
-      a[j].x = __uint_as_float(v[j]);
-      b[j].x = __uint_as_float(v[Q + j]);
-      c[j].x = __uint_as_float(v[2 * Q + j]);
-      d[j].x = __uint_as_float(v[3 * Q + j]);
+      a[j].x = at(j);
+      b[j].x = at(Q + j);
+      c[j].x = at(2 * Q + j);
+      d[j].x = at(3 * Q + j);
     }
+    // PAD: lists c and d (slots KP/2..KP-1) may hold pad rows
+    constexpr int S = PAD ? 0 : 1 << 20;
     sort_full<Q>(a, NanHook<>{nan});
     sort_full<Q>(b, NanHook<>{nan});
-    sort_full<Q>(c, NanHook<>{nan});
-    sort_full<Q>(d, NanHook<>{nan});
+    sort_full<Q>(c, NanHook<1, 0, S>{nan});
+    sort_full<Q>(d, NanHook<1, 0, S>{nan});
     return four_list_median<Q>(a, b, c, d).x;
   } else {
     fx x[KP];
 #pragma unroll
-    for (int j = 0; j < KP; ++j) x[j].x = __uint_as_float(v[j]);
-    run_special<KP, 2>(x, NanHook<>{nan});
+    for (int j = 0; j < KP; ++j) x[j].x = at(j);
+    run_special<KP, 2>(x, NanHook<1, 0, PAD ? KP / 32 : 1 << 20>{nan});  // PAD: blocks of slots >= KP/2
     constexpr int b = (KP * 2) / 10;
     float acc = 0.f;
+    if constexpr (PAD) {  // padded ranks b..b+m-1
+      const int m = K - 2 * trim_b;
+#pragma unroll
+      for (int j = b; j < KP - b; ++j) {
+        if (j - b < m) acc = __fadd_rn(acc, x[j].x);  // a uniform condition
+      }
+      return acc / static_cast<float>(m);
+    }
 #pragma unroll
     for (int j = b; j < KP - b; ++j) acc = __fadd_rn(acc, x[j].x);
     return acc / static_cast<float>(KP - 2 * b);
   }
 }
 
-template <int KP, int RULE, int MODE>
+template <int KP, int RULE, int MODE, bool PAD>
 __device__ __attribute__((noinline)) float robust_coord_keys(const float* const* peers, int K, int trim_b,
                                                              int64_t c0, uint32_t lane_off);
 
@@ -68,7 +93,7 @@ __device__ __attribute__((noinline)) float robust_coord_keys(const float* const*
 // otherwise (K == KP) the float network unless the wave holds a NaN, which
 // re-runs on the keys out of line (re-loading: inlined, LLVM kept both
 // paths' values live, 256 VGPRs and one wave per SIMD).
-template <int KP, int RULE, int MODE, bool KEYS = MODE == 0>
+template <int KP, int RULE, int MODE, bool PAD = false, bool KEYS = MODE == 0>
 __device__ __forceinline__ float robust_coord(const float* const* __restrict__ peers, int K,
                                               int trim_b, int64_t c0, uint32_t lane_off) {
   // Loads are unconditional (a pad slot re-reads peer 0, an L2 hit) so the
@@ -78,25 +103,35 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
   // one 32-bit lane offset shared by every load (no 64-bit VGPR address per
   // load); the asm keeps LLVM from re-associating the tile start into it.
   uint32_t v[KP];
+  const int lo = PAD ? pad_lo(KP, RULE, K, trim_b) : 0;
+  const uint64_t prow = reinterpret_cast<uint64_t>(pad_row(KEYS, false));  // the top row is 512 B on
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
-    const bool real = (MODE != 0) || (j < K);  // MODE 1/2: K == KP
-    uint64_t row = reinterpret_cast<uint64_t>(table_at(peers, real ? j : 0) + c0);
+    const bool real = (MODE != 0 && !PAD) || (PAD && 2 * j < KP) || (j < K);  // PAD: K > KP / 2
+    uint64_t row = reinterpret_cast<uint64_t>(table_at(peers, PAD ? min(j, K - 1) : real ? j : 0) + c0);
+    // PAD: a pad slot reads its pad row (no c0: the row is one tile wide)
+    if (PAD && !real) row = prow + (j - K >= lo ? 512u : 0u);
     asm("" : "+s"(row));
-    v[j] = __float_as_uint(__builtin_nontemporal_load(
-        reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off)));
+    const P2P_GLOBAL float* src =
+        reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off);
+    // a slot that may be a pad loads through the caches (every wave of the
+    // chip reads the same pad rows: streamed, they would all go to one L2
+    // channel); peer rows stream
+    v[j] = __float_as_uint(PAD && 2 * j >= KP ? *src : __builtin_nontemporal_load(src));
   }
   __builtin_amdgcn_sched_barrier(0);  // all KP loads in flight before the first use
   if constexpr (MODE != 0 && !KEYS) {  // K == KP: a NaN-free wave runs on the floats themselves
     uint64_t nan = 0;
-    const float r = special_floats<KP, RULE>(v, nan);
+    const float r = special_floats<KP, RULE, PAD>(v, nan, K, trim_b);
     if (!__builtin_amdgcn_readfirstlane(static_cast<int>(nan != 0))) return r;
-    return robust_coord_keys<KP, RULE, MODE>(peers, K, trim_b, c0, lane_off);
+    return robust_coord_keys<KP, RULE, MODE, PAD>(peers, K, trim_b, c0, lane_off);
   }
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
+    // MODE 0: a pad sorts after every real key; PAD: the pad row's bits map
+    // to the bottom / top key
     const bool real = (MODE != 0) || (j < K);
-    v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;  // pad: sorts after every real key
+    v[j] = real ? f2key(v[j]) : 0xFFFFFFFFu;
   }
   if constexpr (RULE == P2P_RULE_MEDIAN && MODE == 1) {
     // K == KP in {64, 128}: four sorted lists of KP/4 and the two-set search
@@ -140,7 +175,15 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
     }
   } else {
     float acc = 0.f;  // ascending-rank sequential sum from +0
-    if constexpr (MODE == 2) {
+    if constexpr (MODE == 2 && PAD) {
+      constexpr int b = (KP * 2) / 10;  // padded ranks b..b+m-1
+      const int m = K - 2 * trim_b;
+#pragma unroll
+      for (int j = b; j < KP - b; ++j) {
+        if (j - b < m) acc = __fadd_rn(acc, __uint_as_float(key2f(v[j])));  // a uniform condition
+      }
+      return acc / static_cast<float>(m);
+    } else if constexpr (MODE == 2) {
       constexpr int b = (KP * 2) / 10;  // floor(0.2 KP) for KP in {64,128,256}
 #pragma unroll
       for (int j = b; j < KP - b; ++j) acc = __fadd_rn(acc, __uint_as_float(key2f(v[j])));
@@ -158,7 +201,7 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
   }
 }
 
-template <int KP, int RULE, int MODE>
+template <int KP, int RULE, int MODE, bool PAD>
 __device__ __attribute__((noinline)) float robust_coord_keys(const float* const* peers, int K, int trim_b,
                                                              int64_t c0, uint32_t lane_off) {
   // arguments arrive in VGPRs: make the wave-uniform ones scalar again
@@ -166,41 +209,41 @@ __device__ __attribute__((noinline)) float robust_coord_keys(const float* const*
   c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(c0)));
   K = __builtin_amdgcn_readfirstlane(K);
   trim_b = __builtin_amdgcn_readfirstlane(trim_b);
-  return robust_coord<KP, RULE, MODE, true>(peers, K, trim_b, c0, lane_off);
+  return robust_coord<KP, RULE, MODE, PAD, true>(peers, K, trim_b, c0, lane_off);
 }
 
 // ---- kernels ---------------------------------------------------------------
 // KP <= 128 (template arg): one lane per coordinate, 128-lane blocks.
 // P in {2, 4} (GROUP kernels): 128*P-lane blocks.  A block covers kRobustTile
 // coordinates either way.
-template <int KP, int RULE, int MODE>
+template <int KP, int RULE, int MODE, bool PAD>
 __device__ __forceinline__ void robust_one(const float* const* peers, int K, int trim_b, int64_t n,
                                            int64_t tile, float* w, float* out, float lr) {
   const int64_t c0 = tile * kRobustTile;
   const int64_t i = c0 + tid_x();
   if (i >= n) return;
-  const float agg = robust_coord<KP, RULE, MODE>(peers, K, trim_b, c0, tid_x() * 4u);
+  const float agg = robust_coord<KP, RULE, MODE, PAD>(peers, K, trim_b, c0, tid_x() * 4u);
   if (out) stg(out + i, agg);
   if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
 }
 
 // 2-D grid (p2p_common.h tile_grid): tile t = blockIdx.y * gx + blockIdx.x.
-template <int KP, int RULE, int MODE>
+template <int KP, int RULE, int MODE, bool PAD>
 __global__ __launch_bounds__(kRobustTile, MODE != 0 ? 3 : 1) void robust_flat_kernel(
     const float* const* __restrict__ peers, int K, int trim_b, int64_t n, float* w, float* out,
     float lr, int64_t ntiles, unsigned gx) {
   const int64_t t = tile_id(gx);
   if (t >= ntiles) return;
-  robust_one<KP, RULE, MODE>(peers, K, trim_b, n, t, w, out, lr);
+  robust_one<KP, RULE, MODE, PAD>(peers, K, trim_b, n, t, w, out, lr);
 }
 
-template <int KP, int RULE, int MODE>
+template <int KP, int RULE, int MODE, bool PAD>
 __global__ __launch_bounds__(kRobustTile, MODE != 0 ? 3 : 1) void robust_segments_kernel(
     const Seg* __restrict__ segs, int nseg, int K, int trim_b, float lr, int64_t ntiles, unsigned gx) {
   const int64_t t = tile_id(gx);
   if (t >= ntiles) return;
   const Seg s = load_segment(segs, nseg, t);
-  robust_one<KP, RULE, MODE>(s.peers, K, trim_b, s.n, t - s.tile_begin, s.w, s.out, lr);
+  robust_one<KP, RULE, MODE, PAD>(s.peers, K, trim_b, s.n, t - s.tile_begin, s.w, s.out, lr);
 }
 
 struct RobustArgs {
@@ -216,28 +259,36 @@ struct RobustArgs {
   hipStream_t stream;
 };
 
-template <int KP, int RULE, int MODE>
+template <int KP, int RULE, int MODE, bool PAD = false>
 static void launch_one(const RobustArgs& a) {
   const int64_t tiles = a.segs ? a.tiles : ceil_div(a.n, kRobustTile);
   const TileGrid g = tile_grid(tiles);
   if (g.gx == 0) return;
   if (a.segs) {
-    hipLaunchKernelGGL((robust_segments_kernel<KP, RULE, MODE>), dim3(g.gx, g.gy), dim3(kRobustTile), 0, a.stream,
+    hipLaunchKernelGGL((robust_segments_kernel<KP, RULE, MODE, PAD>), dim3(g.gx, g.gy), dim3(kRobustTile), 0, a.stream,
                        a.segs, a.nseg, a.K, a.trim_b, a.lr, tiles, g.gx);
   } else {
-    hipLaunchKernelGGL((robust_flat_kernel<KP, RULE, MODE>), dim3(g.gx, g.gy), dim3(kRobustTile), 0, a.stream,
+    hipLaunchKernelGGL((robust_flat_kernel<KP, RULE, MODE, PAD>), dim3(g.gx, g.gy), dim3(kRobustTile), 0, a.stream,
                        a.peers, a.K, a.trim_b, a.n, a.w, a.out, a.lr, tiles, g.gx);
   }
+}
+
+// The pads fit a K < KP (or another trim) into the K == KP networks: the
+// median always; the trimmed mean while b <= b0, K - b <= KP - b0 and
+// m = K - 2b <= KP - 2 b0 (every K in 33..128 at the default 0.2 trim).
+static bool robust_pad_fits(int KP, int rule, int K, int b) {
+  if (K > KP || 2 * K <= KP) return false;
+  if (rule == P2P_RULE_MEDIAN) return true;
+  const int b0 = (KP * 2) / 10;
+  return b >= 0 && b <= b0 && K - b <= KP - b0 && K - 2 * b >= 1 && K - 2 * b <= KP - 2 * b0;
 }
 
 template <int KP, int RULE>
 static void launch_kp(const RobustArgs& a) {
   if constexpr (KP == 64 || KP == 128) {
-    if constexpr (RULE == P2P_RULE_MEDIAN) {
-      if (a.K == KP) return launch_one<KP, RULE, 1>(a);
-    } else {
-      if (a.K == KP && a.trim_b == (KP * 2) / 10) return launch_one<KP, RULE, 2>(a);
-    }
+    constexpr int MODE = RULE == P2P_RULE_MEDIAN ? 1 : 2;
+    if (a.K == KP && (RULE == P2P_RULE_MEDIAN || a.trim_b == (KP * 2) / 10)) return launch_one<KP, RULE, MODE>(a);
+    if (robust_pad_fits(KP, RULE, a.K, a.trim_b)) return launch_one<KP, RULE, MODE, true>(a);
   }
   launch_one<KP, RULE, 0>(a);
 }

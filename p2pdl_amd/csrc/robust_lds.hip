@@ -649,25 +649,26 @@ extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t rule, int32_t k) {
   return LdsLayout<4, 64>::TB;
 }
 
+extern "C" P2P_INTERNAL int32_t p2p_robust_pair_fits(int32_t rule, int32_t k, int32_t trim_b);
 extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, const p2p_segment_t* segs,
-                                                    int32_t nseg, int64_t tiles, int32_t rule, int64_t n,
-                                                    float* w, float* out, float lr, p2p_stream_t stream);
+                                                    int32_t nseg, int64_t tiles, int32_t rule, int32_t k,
+                                                    int32_t trim_b, int64_t n, float* w, float* out, float lr,
+                                                    p2p_stream_t stream);
 
-// K = 256 with the default trim (the pruned networks): one lane per
-// coordinate in two-wave blocks, robust_pair.hip.  Any other K in 129..255 or trim runs the generic
-// padded network -- ~1.4x the instructions -- where two sorter groups per
-// block are faster (median -7%, trimmed -12% time for K in 129..255, round-2
-// lab A/B, profiles/r02/ab/labg2k); for the pruned K = 256 networks the
-// single-buffered images of the two-group block expose the DMA (median +27%).
+// K in 129..256 with the median or a trim the pads fit (every K at the
+// default 0.2): one lane per coordinate in two-wave blocks, robust_pair.hip,
+// the block padded to 256 (round 4; 2-3x faster than these LDS kernels at
+// K = 200).  Any other trim runs the generic padded network here, where two
+// sorter groups per block were faster than one (round-2 lab A/B,
+// profiles/r02/ab/labg2k).
 extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, const p2p_segment_t* segs,
                                                    int32_t nseg, int64_t tiles, int32_t k, int32_t rule,
                                                    int32_t trim_b, int64_t n, float* w, float* out, float lr,
                                                    p2p_stream_t stream) {
   LdsArgs a{peers, segs, nseg, tiles, k, trim_b, n, w, out, lr, static_cast<hipStream_t>(stream)};
   const bool med = rule == P2P_RULE_MEDIAN;
-  const bool pruned = k == 256 && (med || trim_b == (256 * 2) / 10);
-  if (pruned) {
-    p2p_robust_pair_launch(peers, segs, nseg, tiles, rule, n, w, out, lr, stream);
+  if (p2p_robust_pair_fits(rule, k, trim_b)) {
+    p2p_robust_pair_launch(peers, segs, nseg, tiles, rule, k, trim_b, n, w, out, lr, stream);
   } else if (med) {
     if (segs) launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, true>(a); else launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, false>(a);
   } else {

@@ -46,10 +46,30 @@ __device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) {
   asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
 }
-template <int N, typename F>
+// v_maximum3_f32 (IEEE 754-2019 maximum, gfx950): NaN in, NaN out, and no
+// NaN from infinities.
+__device__ __forceinline__ float maximum3(float a, float b, float c) {
+  float d;
+  asm volatile("v_maximum3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+// INF_SAFE: the test of a padded network's slots, whose +-inf pad rows meet
+// (inf - inf in the FMA chain would send every tile to the key path): two
+// v_maximum3 chains, two values per instruction.
+template <int N, bool INF_SAFE = false, typename F>
 __device__ __forceinline__ uint64_t nan_lanes(F&& at) {
   static_assert(N % 2 == 0, "pairs");
-  if constexpr (N < 6) {
+  if constexpr (INF_SAFE && N >= 6) {
+    float a = maximum3(at(0), at(1), at(2)), b = maximum3(at(3), at(4), at(5));
+    int j = 6;
+#pragma unroll
+    for (; j + 3 < N; j += 4) {
+      a = maximum3(a, at(j), at(j + 1));
+      b = maximum3(b, at(j + 2), at(j + 3));
+    }
+    if constexpr ((N - 6) % 4 == 2) a = maximum3(a, at(N - 2), at(N - 1));
+    return unordered_mask(a, b);
+  } else if constexpr (N < 6) {
     uint64_t m = 0;
 #pragma unroll
     for (int j = 0; j < N / 2; ++j) m |= unordered_mask(at(j), at(j + N / 2));
@@ -104,6 +124,24 @@ __device__ __forceinline__ void ce(fx& a, fx& b) {
       __builtin_amdgcn_bitop3_b32(__float_as_uint(a.x), __float_as_uint(b.x), __float_as_uint(lo), 0x96));
   if constexpr (ASC) { a.x = lo; b.x = hi; } else { a.x = hi; b.x = lo; }
 }
+// Pad rows of the padded robust kernels (K below the network's size): a pad
+// slot loads lane l's word from one of these 128-word rows instead of a peer
+// row -- L1/L2-resident, no HBM traffic, no VALU select -- so the network
+// sees -inf / +inf (float path) or the bottom / top key (key path: float bits
+// 0xFFFFFFFF and 0x7FFFFFFF, which f2key maps to 0 and ~0).
+#define P2P_R4(x) x, x, x, x
+#define P2P_R16(x) P2P_R4(x), P2P_R4(x), P2P_R4(x), P2P_R4(x)
+#define P2P_R128(x) P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x)
+__device__ static const uint32_t kPadRows[4][128] = {{P2P_R128(0xFF800000u)}, {P2P_R128(0x7F800000u)},
+                                                     {P2P_R128(0xFFFFFFFFu)}, {P2P_R128(0x7FFFFFFFu)}};
+#undef P2P_R128
+#undef P2P_R16
+#undef P2P_R4
+// The pad row for (key path?, top of the order?), as a peer row pointer.
+__device__ __forceinline__ const float* pad_row(bool keys, bool top) {
+  return reinterpret_cast<const float*>(kPadRows[(keys ? 2 : 0) + (top ? 1 : 0)]);
+}
+
 // Per-block hook of the generated networks: hook(v, blk) runs before the
 // first comparator that reads keys 16*blk .. 16*blk+15 (still the inputs).
 struct NoHook {
@@ -117,15 +155,17 @@ __device__ __forceinline__ float bits_f(fx x) { return x.x; }
 // block as the network first reads it: the test waits only for that
 // block's loads (a whole-wave test up front waited for every load before the
 // first comparator: median256 -3.5% time without it).
-// G blocks per test, blocks from FIRST on.
-template <int G = 1, int FIRST = 0>
+// G blocks per test, blocks from FIRST on; blocks from SAFE on may hold pad
+// rows (nan_lanes INF_SAFE).
+template <int G = 1, int FIRST = 0, int SAFE = 1 << 20>
 struct NanHook {
   uint64_t& m;
   template <typename T, int KP>
   __device__ __forceinline__ void operator()(T (&v)[KP], int blk) const {
     if (blk % G != 0 || blk < FIRST) return;
     constexpr int N = 16 * G < KP ? 16 * G : KP;
-    m |= nan_lanes<N>([&](int j) { return bits_f(v[16 * blk + j]); });
+    if (blk >= SAFE) m |= nan_lanes<N, true>([&](int j) { return bits_f(v[16 * blk + j]); });
+    else m |= nan_lanes<N>([&](int j) { return bits_f(v[16 * blk + j]); });
   }
 };
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {

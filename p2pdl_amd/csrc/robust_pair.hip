@@ -110,18 +110,34 @@ __device__ __forceinline__ void pin(const T (&x)[N]) {
   for (int j = 0; j < N; ++j) asm volatile("" ::"v"(raw(x[j])));
 }
 
+// K in 129..255 (PAD kernels): the block sorts a padded 256 -- wave h holds
+// slots 128h..128h+127, slots >= K are pads, the first `lo` of them at the
+// bottom of the order and the rest at the top (+-inf on the float path,
+// keys 0 / ~0 on the key path: every real key orders between them, ties
+// are the same value).  The median takes lo = 127 - (K-1)/2, so rank 127 of
+// the 256 is the real lower median; the trimmed mean lo = 51 - b, so the
+// kept real ranks b..K-b-1 are padded ranks 51..51+m-1 (m = K - 2b <= 154)
+// and the sum stops after m of them.  A pad slot loads its word from a pad
+// row (robust_nets.h pad_row: the row is one tile wide, so the PAD kernels
+// keep the tile start in the row base, not in the lane offset).
+struct Pads {
+  int kr = kHalf;  // real slots in this wave
+  int lo = 0;      // low pads
+  int m = 2 * kHalf - 2 * 51;  // trimmed: kept ranks
+};
+
 // NaN test of N consecutive loaded keys (robust_nets.h nan_lanes).
-template <int N>
+template <int N, bool INF_SAFE = false>
 __device__ __forceinline__ uint64_t list_nan_mask(const uint32_t* v) {
-  return nan_lanes<N>([&](int j) { return __uint_as_float(v[j]); });
+  return nan_lanes<N, INF_SAFE>([&](int j) { return __uint_as_float(v[j]); });
 }
 
 // One half sorted in T's domain (the block's: keys if either half holds a
 // NaN); returns the aggregate, valid in wave 0.  Both waves pass the same
 // number of block barriers.
-template <int RULE>
+template <int RULE, bool PAD>
 __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int64_t c0, uint32_t lane_off, Img im,
-                                                     int h, int lane);
+                                                     int h, int lane, int K, int kr, int lo, int m);
 
 // MEDIAN (rank 127 of 256) without sorting the halves: wave h sorts its
 // peers as two lists of 64 (p = peers 128h..128h+63, q = the next 64) and
@@ -133,20 +149,21 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
 // two-set search (robust_nets.h).  Against two Batcher sorts of 128 and the
 // flip this issues 17% fewer VALU instructions per coordinate; the 16 KB
 // image leaves room for 3 blocks' worth of waves per SIMD pair.
-template <typename T, bool FLAGS = false>
+template <typename T, bool FLAGS = false, bool PAD = false>
 __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im, int h, int lane,
                                              int __attribute__((address_space(3)))* flags = nullptr,
-                                             const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0) {
+                                             const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0,
+                                             int K = 2 * kHalf, const Pads& pd = Pads{}) {
   constexpr int Q = kHalf / 2;  // 64 keys per sorted list
   // FLAGS: each list's NaN test right before its sort, so sorting p overlaps
   // q's loads (a test of all 128 up front waited for every load: +3.5% time)
   T p[Q], q[Q];
   uint64_t nan = 0;
-  if constexpr (FLAGS) nan = list_nan_mask<Q>(v);
+  if constexpr (FLAGS) nan = list_nan_mask<Q, PAD>(v);
 #pragma unroll
   for (int j = 0; j < Q; ++j) p[j] = from_bits<T>(v[j]);
   sort_full<Q>(p);
-  if constexpr (FLAGS) nan |= list_nan_mask<Q>(v + Q);
+  if constexpr (FLAGS) nan |= list_nan_mask<Q, PAD>(v + Q);
 #pragma unroll
   for (int j = 0; j < Q; ++j) q[j] = from_bits<T>(v[Q + j]);
   sort_full<Q>(q);
@@ -165,7 +182,8 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
   }
   block_sync();  // 1: both max(lo)
   if constexpr (FLAGS) {
-    if (uniform((flags[0] | flags[1]) != 0)) return pair_keys<P2P_RULE_MEDIAN>(P, c0, lane_off, im, h, lane);
+    if (uniform((flags[0] | flags[1]) != 0))
+      return pair_keys<P2P_RULE_MEDIAN, PAD>(P, c0, lane_off, im, h, lane, K, pd.kr, pd.lo, pd.m);
   }
   const T mo = from_raw<T>(part[(1 - h) * 64 + lane]);
   const bool d = h == 0 ? le(m, mo) : le(mo, m);  // max(A_lo) <= max(B_lo): A_hi u B_lo
@@ -189,10 +207,11 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
 // FLAGS (float path): the two waves swap "my half holds a NaN" at barrier 1,
 // beside the hand-off; a block that finds one re-runs the tile on the key
 // network (pair_keys) -- the float sort of a NaN half is discarded.
-template <int RULE, typename T, bool FLAGS = false>
+template <int RULE, typename T, bool FLAGS = false, bool PAD = false>
 __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, int h, int lane,
                                            int __attribute__((address_space(3)))* flags = nullptr,
-                                           const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0) {
+                                           const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0,
+                                           int K = 2 * kHalf, const Pads& pd = Pads{}) {
   T x[kHalf];
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) x[j] = from_bits<T>(v[j]);
@@ -201,8 +220,8 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   // overlaps the last loads
   uint64_t nan = 0;
   if constexpr (FLAGS) {
-    nan = list_nan_mask<kHalf / 2>(v);
-    sort_full<kHalf>(x, NanHook<4, 4>{nan});
+    nan = list_nan_mask<kHalf / 2, PAD>(v);
+    sort_full<kHalf>(x, NanHook<4, 4, PAD ? 0 : 1 << 20>{nan});
   } else {
     sort_full<kHalf>(x);
   }
@@ -231,7 +250,8 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   }
   block_sync();  // 1: both parities in the image
   if constexpr (FLAGS) {
-    if (uniform((flags[0] | flags[1]) != 0)) return pair_keys<RULE>(P, c0, lane_off, im, h, lane);
+    if (uniform((flags[0] | flags[1]) != 0))
+      return pair_keys<RULE, PAD>(P, c0, lane_off, im, h, lane, K, pd.kr, pd.lo, pd.m);
   }
   {
     constexpr int b = (2 * kHalf * 2) / 10;  // 51: ranks b..2*kHalf-b-1 = 51..204 kept
@@ -276,7 +296,10 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
       c[2 * (IM - I0)] = min(from_raw<T>(row_at(r1, IM - I0, lane)), m[IM - 1]);
       float acc = 0.f;
 #pragma unroll
-      for (int k = 0; k < 2 * (IM - I0) + 1; ++k) acc = __fadd_rn(acc, val(c[k]));
+      for (int k = 0; k < 2 * (IM - I0) + 1; ++k) {
+        const float s = __fadd_rn(acc, val(c[k]));
+        acc = !PAD || k < pd.m ? s : acc;  // PAD: padded rank b + k is kept iff k < m
+      }
       part[lane] = acc;
       block_sync();  // 3: the partial sum of ranks 51..127 in its slot
       return 0.f;
@@ -292,7 +315,11 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
     block_sync();  // 3
     float acc = part[lane];
 #pragma unroll
-    for (int k = 0; k < 2 * (I1 - IM) + 1; ++k) acc = __fadd_rn(acc, val(c[k]));
+    for (int k = 0; k < 2 * (I1 - IM) + 1; ++k) {
+      const float s = __fadd_rn(acc, val(c[k]));
+      acc = !PAD || 2 * (IM - I0) + 1 + k < pd.m ? s : acc;  // padded rank b + 77 + k
+    }
+    if constexpr (PAD) return acc / static_cast<float>(pd.m);
     return acc / static_cast<float>(2 * kHalf - 2 * b);
   }
 }
@@ -301,14 +328,23 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
 // peer row's base plus the tile start in SGPRs, one 32-bit lane offset shared
 // by all 128 loads -- no 64-bit VGPR address per load.  The asm keeps LLVM
 // from re-associating the tile start into the lane offset.
+// PAD: slots >= K read their pad row (KEYS: the key path's), lo of them the
+// bottom one.
+template <bool PAD = false, bool KEYS = false>
 __device__ __forceinline__ void load_half(uint32_t (&v)[kHalf], const float* const* P, int64_t c0,
-                                          uint32_t lane_off, int h) {
+                                          uint32_t lane_off, int h, int K = 2 * kHalf, int lo = 0) {
+  const uint64_t prow = reinterpret_cast<uint64_t>(pad_row(KEYS, false));  // the top row is 512 B on
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) {
-    uint64_t row = reinterpret_cast<uint64_t>(table_at(P, h * kHalf + j) + c0);
+    const int slot = h * kHalf + j;
+    uint64_t row = reinterpret_cast<uint64_t>(table_at(P, PAD ? min(slot, K - 1) : slot) + c0);
+    if (PAD && slot >= K) row = prow + (slot - K >= lo ? 512u : 0u);
     asm("" : "+s"(row));
-    v[j] = __float_as_uint(__builtin_nontemporal_load(
-        reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off)));
+    const P2P_GLOBAL float* src =
+        reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off);
+    // PAD: through the caches (every wave of the chip reads the same pad
+    // rows: streamed, they would all go to one L2 channel)
+    v[j] = __float_as_uint(PAD ? *src : __builtin_nontemporal_load(src));
   }
   __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first use
 }
@@ -316,27 +352,32 @@ __device__ __forceinline__ void load_half(uint32_t (&v)[kHalf], const float* con
 // The uint32-key network for a block holding a NaN.  Out of line and
 // re-loading its inputs, so the float path's 128 values are not also held
 // live for this one (inlined, the two paths took 320-390 VGPRs).
-template <int RULE>
+template <int RULE, bool PAD>
 __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int64_t c0, uint32_t lane_off, Img im,
-                                                     int h, int lane) {
+                                                     int h, int lane, int K, int kr, int lo, int m) {
   // arguments arrive in VGPRs: make the wave-uniform ones scalar again
   P = reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(P)));
   c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(c0)));
   h = __builtin_amdgcn_readfirstlane(h);
+  Pads pd;
+  pd.kr = __builtin_amdgcn_readfirstlane(kr);
+  pd.lo = __builtin_amdgcn_readfirstlane(lo);
+  pd.m = __builtin_amdgcn_readfirstlane(m);
+  K = __builtin_amdgcn_readfirstlane(K);
   uint32_t v[kHalf];
-  load_half(v, P, c0, lane_off, h);
-  if constexpr (RULE == P2P_RULE_MEDIAN) return median_pair<uint32_t>(v, im, h, lane);
-  else return pair_body<RULE, kx>(v, im, h, lane);  // kx: max as a ^ b ^ min, fewer live values
+  load_half<PAD, true>(v, P, c0, lane_off, h, K, pd.lo);
+  if constexpr (RULE == P2P_RULE_MEDIAN) return median_pair<uint32_t, false, PAD>(v, im, h, lane, nullptr, P, c0, lane_off, K, pd);
+  else return pair_body<RULE, kx, false, PAD>(v, im, h, lane, nullptr, P, c0, lane_off, K, pd);  // kx: max as a ^ b ^ min
 }
 
 // One 64-coordinate tile of the pair kernels.  SMALL (flat buffers below
 // 2^30 floats): the tile start rides in the 32-bit lane offset and each peer
 // row's pointer is the scalar base as loaded -- no 64-bit scalar add per load
 // (256 SALU instructions per wave and tile).
-template <int RULE, bool SEGS, bool SMALL>
+template <int RULE, bool SEGS, bool SMALL, bool PAD>
 __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers, const Seg* __restrict__ segs,
                                           int nseg, int64_t n, float* w, float* out, float lr, Img im,
-                                          int __attribute__((address_space(3)))* flags, int64_t t) {
+                                          int __attribute__((address_space(3)))* flags, int64_t t, int K, int trim_b) {
   const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
   const int lane = tid_x() & 63;
   const float* const* P = peers;
@@ -353,15 +394,23 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
   }
   const int64_t i = c0 + lane;
   // Dead lanes of a ragged tail re-read the last element.
-  const int64_t cb = SMALL ? 0 : c0;  // row base offset (0: the whole offset rides per lane)
+  // row base offset (SMALL: 0, the whole offset rides per lane; never for
+  // PAD, whose pad rows are one tile wide)
+  const int64_t cb = SMALL && !PAD ? 0 : c0;
   const uint32_t lane_off = static_cast<uint32_t>((i < N ? i : N - 1) - cb) * 4u;
+  Pads pd;
+  if constexpr (PAD) {
+    pd.kr = h == 0 ? kHalf : K - kHalf;
+    pd.lo = RULE == P2P_RULE_MEDIAN ? (2 * kHalf - 1) / 2 - (K - 1) / 2 : (2 * kHalf * 2) / 10 - trim_b;
+    pd.m = K - 2 * trim_b;
+  }
   uint32_t v[kHalf];
-  load_half(v, P, cb, lane_off, h);
+  load_half<PAD>(v, P, cb, lane_off, h, K, pd.lo);
   // One domain per block: the float network unless either half holds a NaN
   // (flags swapped at the first barrier, no barrier of their own).
   float agg;
-  if constexpr (RULE == P2P_RULE_MEDIAN) agg = median_pair<fk, true>(v, im, h, lane, flags, P, cb, lane_off);
-  else agg = pair_body<RULE, fk, true>(v, im, h, lane, flags, P, cb, lane_off);
+  if constexpr (RULE == P2P_RULE_MEDIAN) agg = median_pair<fk, true, PAD>(v, im, h, lane, flags, P, cb, lane_off, K, pd);
+  else agg = pair_body<RULE, fk, true, PAD>(v, im, h, lane, flags, P, cb, lane_off, K, pd);
   if (h == 0 && i < N) {  // wave 0 holds the aggregate
     if (O) stg(O + i, agg);
     if (W) stg(W + i, apply_lr(ldg(W + i), lr, agg));
@@ -370,56 +419,75 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
 
 // Trimmed mean: two 16 KB parity regions + the partial sums (256 B), 2 waves
 // per SIMD.
-template <bool SEGS, bool SMALL = false>
+template <bool SEGS, bool SMALL = false, bool PAD = false>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(
     const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n, float* w,
-    float* out, float lr, int64_t ntiles, unsigned gx) {
+    float* out, float lr, int64_t ntiles, unsigned gx, int K, int trim_b) {
   __shared__ u32x4 img_raw[kHalf / 4 * 64 + 16];
   __shared__ int nan_flag[2];
   const int64_t t = tile_id(gx);
   if (t >= ntiles) return;  // block-uniform
-  pair_tile<P2P_RULE_TRIMMED, SEGS, SMALL>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
-                                           (int __attribute__((address_space(3)))*)nan_flag, t);
+  pair_tile<P2P_RULE_TRIMMED, SEGS, SMALL, PAD>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
+                                                (int __attribute__((address_space(3)))*)nan_flag, t, K, trim_b);
 }
 
 // Median: 16 KB image (B's kept half) + both max(lo) (512 B), 3 waves per
 // SIMD (<= 168 VGPRs).
-template <bool SEGS, bool SMALL = false>
+template <bool SEGS, bool SMALL = false, bool PAD = false>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void robust_median_pair_kernel(
     const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n, float* w,
-    float* out, float lr, int64_t ntiles, unsigned gx) {
+    float* out, float lr, int64_t ntiles, unsigned gx, int K, int trim_b) {
   __shared__ u32x4 img_raw[kHalf / 8 * 64 + 32];
   __shared__ int nan_flag[2];
   const int64_t t = tile_id(gx);
   if (t >= ntiles) return;  // block-uniform
-  pair_tile<P2P_RULE_MEDIAN, SEGS, SMALL>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
-                                          (int __attribute__((address_space(3)))*)nan_flag, t);
+  pair_tile<P2P_RULE_MEDIAN, SEGS, SMALL, PAD>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
+                                               (int __attribute__((address_space(3)))*)nan_flag, t, K, trim_b);
 }
 
 }  // namespace p2p
 
 using namespace p2p;
 
-// K = 256, median or trimmed with b = 51: one block per 64-coordinate tile
+// Whether the pair kernels take (rule, K, b): K = 256 with the median or
+// b = 51 as built; K in 129..255 (or another b) padded to 256 when the pads
+// fit (the median always; the trimmed mean while b <= 51, K - b <= 205 and
+// K - 2b <= 154, which every K in 129..256 meets at the default 0.2 trim).
+extern "C" P2P_INTERNAL int32_t p2p_robust_pair_fits(int32_t rule, int32_t k, int32_t trim_b) {
+  if (k <= kHalf || k > 2 * kHalf) return 0;
+  if (rule == P2P_RULE_MEDIAN) return 1;
+  return trim_b >= 0 && trim_b <= 51 && k - trim_b <= 205 && k - 2 * trim_b >= 1 && k - 2 * trim_b <= 154;
+}
+
+// K in 129..256 (p2p_robust_pair_fits): one block per 64-coordinate tile
 // (flat: ceil(n / 64); segment table: `tiles`, tile_begin in units of 64), on
-// a 2-D grid beyond 2^24 tiles.
+// a 2-D grid beyond 2^24 tiles.  The unpadded kernels for K = 256 with the
+// median or b = 51, the PAD kernels otherwise.
 extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, const p2p_segment_t* segs,
-                                                    int32_t nseg, int64_t tiles, int32_t rule, int64_t n,
-                                                    float* w, float* out, float lr, p2p_stream_t stream) {
+                                                    int32_t nseg, int64_t tiles, int32_t rule, int32_t k,
+                                                    int32_t trim_b, int64_t n, float* w, float* out, float lr,
+                                                    p2p_stream_t stream) {
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t ntiles = segs ? tiles : ceil_div(n, kPairTile);
   const TileGrid tg = tile_grid(ntiles);  // 2 x 64 lanes per 64 coordinates: 1-D, n > 2^31 would wrap
   if (tg.gx == 0) return;
   const dim3 g(tg.gx, tg.gy), b(2 * 64);
-#define P2P_PAIR_ARGS g, b, 0, st, peers, segs, nseg, n, w, out, lr, ntiles, tg.gx
-  if (rule == P2P_RULE_MEDIAN) {
-    if (segs) hipLaunchKernelGGL((robust_median_pair_kernel<true>), P2P_PAIR_ARGS);
-    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_median_pair_kernel<false, true>), P2P_PAIR_ARGS);
-    else hipLaunchKernelGGL((robust_median_pair_kernel<false>), P2P_PAIR_ARGS);
-  } else {
-    if (segs) hipLaunchKernelGGL((robust_pair_kernel<true>), P2P_PAIR_ARGS);
-    else if (n <= (int64_t(1) << 30)) hipLaunchKernelGGL((robust_pair_kernel<false, true>), P2P_PAIR_ARGS);
-    else hipLaunchKernelGGL((robust_pair_kernel<false>), P2P_PAIR_ARGS);
-  }
+  const bool pad = !(k == 2 * kHalf && (rule == P2P_RULE_MEDIAN || trim_b == 51));
+  const bool small = !segs && n <= (int64_t(1) << 30);
+#define P2P_PAIR_ARGS g, b, 0, st, peers, segs, nseg, n, w, out, lr, ntiles, tg.gx, k, trim_b
+#define P2P_PAIR_LAUNCH(KERNEL)                                                                \
+  do {                                                                                         \
+    if (pad) {                                                                                 \
+      if (segs) hipLaunchKernelGGL((KERNEL<true, false, true>), P2P_PAIR_ARGS);                \
+      else hipLaunchKernelGGL((KERNEL<false, false, true>), P2P_PAIR_ARGS);                    \
+    } else {                                                                                   \
+      if (segs) hipLaunchKernelGGL((KERNEL<true, false, false>), P2P_PAIR_ARGS);               \
+      else if (small) hipLaunchKernelGGL((KERNEL<false, true, false>), P2P_PAIR_ARGS);         \
+      else hipLaunchKernelGGL((KERNEL<false, false, false>), P2P_PAIR_ARGS);                   \
+    }                                                                                          \
+  } while (0)
+  if (rule == P2P_RULE_MEDIAN) P2P_PAIR_LAUNCH(robust_median_pair_kernel);
+  else P2P_PAIR_LAUNCH(robust_pair_kernel);
+#undef P2P_PAIR_LAUNCH
 #undef P2P_PAIR_ARGS
 }

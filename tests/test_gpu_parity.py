@@ -436,12 +436,14 @@ def nan_free_special_peers(k, n, seed):
 
 
 @pytest.mark.parametrize("rule", ["median", "trimmed"])
-@pytest.mark.parametrize("k", [64, 128, 256])
+@pytest.mark.parametrize("k", [33, 64, 65, 100, 127, 128, 129, 200, 255, 256])
 @pytest.mark.parametrize("nan_stripe", [False, True])
 def test_robust_float_fast_path_specials(cuda, rule, k, nan_stripe):
-    """K == KP with b = floor(0.2 K): NaN-free waves run the float network,
-    a wave holding one NaN runs the uint32-key network; both bit-exact with
-    the oracle (median: the selected bits, so -0 vs +0 included)."""
+    """b = floor(0.2 K) at K == KP and at K padded up to KP (pad rows at both
+    ends of the order): NaN-free waves run the float network, a wave holding
+    one NaN runs the uint32-key network; both bit-exact with the oracle
+    (median: the selected bits, so -0 vs +0 included) -- +-inf inputs tie
+    with the pads."""
     n = 40_003
     peers = nan_free_special_peers(k, n, 13 * k + int(nan_stripe))
     if nan_stripe:  # one NaN in every 997th coordinate: those waves take the key path
@@ -458,7 +460,7 @@ def test_robust_float_fast_path_specials(cuda, rule, k, nan_stripe):
 
 
 @pytest.mark.parametrize("rule", ["median", "trimmed"])
-@pytest.mark.parametrize("k", [16, 64, 128, 200, 256])
+@pytest.mark.parametrize("k", [16, 64, 100, 128, 200, 256])
 def test_robust_single_nan_at_every_peer_position(cuda, rule, k):
     """The float networks' NaN test (robust_nets.h nan_lanes: packed-FMA
     chains ended by one compare) must see a NaN wherever it sits: tile t
@@ -485,7 +487,10 @@ def test_robust_single_nan_at_every_peer_position(cuda, rule, k):
     assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k} one NaN per tile")
 
 
-@pytest.mark.parametrize("k,b", [(5, 0), (5, 2), (10, 3), (128, 0), (128, 63), (200, 10), (256, 51), (256, 100)])
+@pytest.mark.parametrize("k,b", [(5, 0), (5, 2), (10, 3), (128, 0), (128, 63), (200, 10), (256, 51), (256, 100),
+                                 # padded networks with another trim: (65, 0), (100, 15), (129, 0),
+                                 # (150, 51), (200, 40); outside the pads' fit: (100, 10), (256, 40)
+                                 (65, 0), (100, 15), (129, 0), (150, 51), (200, 40), (100, 10), (256, 40)])
 def test_trimmed_explicit_b(cuda, k, b):
     n = 1000
     peers = [oracle.synth(n, k + b, p, 1.0) for p in range(k)]
@@ -535,7 +540,7 @@ def structured_peers(k, seed):
 
 
 @pytest.mark.parametrize("rule", ["median", "trimmed"])
-@pytest.mark.parametrize("k", [64, 128, 256])
+@pytest.mark.parametrize("k", [64, 100, 128, 200, 256])
 def test_robust_structured_extremes(cuda, rule, k):
     """The pair kernel's parity merge / two-set search and the one-lane
     networks on inputs that push every merge to an extreme (bit-exact)."""
