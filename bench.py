@@ -82,6 +82,10 @@ WORKLOADS = {
     "trimmed200": ("trimmed", 200, 100_000_000, 0x5EED0009),
     "median96": ("median", 96, 100_000_000, 0x5EED000A),
     "trimmed96": ("trimmed", 96, 100_000_000, 0x5EED000A),
+    "median24": ("median", 24, 100_000_000, 0x5EED000B),
+    "trimmed24": ("trimmed", 24, 100_000_000, 0x5EED000B),
+    "median32": ("median", 32, 100_000_000, 0x5EED000B),
+    "trimmed32": ("trimmed", 32, 100_000_000, 0x5EED000B),
     # cfg5: 256 serialized updates (64-B header + 25M fp32 payload), digest all,
     # reject the ~10% whose bytes were corrupted, FedAvg the accepted ones
     "cfg5": ("fused", 256, 25_000_000, 0x5EED0004),

@@ -14,7 +14,8 @@
 // checked) by gen_networks.py into networks.inc.
 //
 // K <= 128: ONE LANE per coordinate (KP = next power of two, +inf pads; a
-// network pruned to the wanted ranks when K == KP in {64, 128}).  The float
+// network pruned to the wanted ranks when K == KP in {64, 128}, and for any
+// K in 33..127 padded at both ends of the order into those networks -- PAD).  The float
 // network of robust_nets.h is NOT used here: holding the float copy next to
 // the keys took the K = 128 kernels from 146 / 183 VGPRs (3 / 2 waves per
 // SIMD) to 256 (1 wave) and cfg4 from 73% / 60% to 59% / 52% of HBM peak.  Loads:
