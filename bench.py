@@ -79,6 +79,7 @@ WORKLOADS = {
     # K between the kernel families' sizes: the 4-lanes-per-coordinate LDS
     # kernels (K 129..255); not a BASELINE config, run on request only
     "median200": ("median", 200, 100_000_000, 0x5EED0009),
+    "median160": ("median", 160, 100_000_000, 0x5EED0009),
     "trimmed200": ("trimmed", 200, 100_000_000, 0x5EED0009),
     "median96": ("median", 96, 100_000_000, 0x5EED000A),
     "trimmed96": ("trimmed", 96, 100_000_000, 0x5EED000A),

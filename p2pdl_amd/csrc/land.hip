@@ -85,7 +85,7 @@ extern "C" int32_t p2p_land_segments_f32(const uint8_t* msg, uint64_t msg_bytes,
                                          int32_t nseg, int64_t total_tiles, p2p_stream_t stream) {
   if (!msg || !segs || nseg < 1 || total_tiles < 0) return P2P_ERR_INVALID;
   if (total_tiles == 0) return P2P_OK;
-  const TileGrid tg = tile_grid(total_tiles);
+  const TileGrid tg = tile_grid(total_tiles, kBlock);
   hipLaunchKernelGGL(land_segments_kernel, dim3(tg.gx, tg.gy), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
                      msg, msg_bytes, segs, nseg, total_tiles, tg.gx);
   return static_cast<int32_t>(hipGetLastError());

@@ -108,13 +108,15 @@ __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + 
 // 32 bits per dimension: one 128-lane block per 64 or 128 coordinates in x
 // alone would wrap past 2^31 / 2^32 coordinates and leave the rest of the
 // buffer untouched.  Tile t = blockIdx.y * gx + blockIdx.x with gx <= 2^24
-// blocks; the surplus blocks of the last row exit at once.
+// blocks of 128 lanes (2^31 work-items per row; fewer blocks for larger
+// ones); the surplus blocks of the last row exit at once.
 constexpr int64_t kMaxGridX = int64_t(1) << 24;
 struct TileGrid {
   unsigned gx, gy;
 };
-__host__ inline TileGrid tile_grid(int64_t tiles) {
-  const int64_t gx = tiles < kMaxGridX ? tiles : kMaxGridX;
+__host__ inline TileGrid tile_grid(int64_t tiles, int block = 128) {
+  const int64_t cap = block <= 128 ? kMaxGridX : (int64_t(1) << 31) / block;
+  const int64_t gx = tiles < cap ? tiles : cap;
   return TileGrid{static_cast<unsigned>(gx), static_cast<unsigned>(gx > 0 ? ceil_div(tiles, gx) : 0)};
 }
 __device__ __forceinline__ int64_t tile_id(unsigned gx) {

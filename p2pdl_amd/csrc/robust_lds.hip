@@ -643,10 +643,14 @@ using namespace p2p;
 // size is a pure function of (rule, k)).  Other
 // instantiations of the templates above (4 x 32, 2 x 64, 1 x 128, 2 x 128)
 // are built only into the A/B library of tools/robust_lab.hip.
+extern "C" P2P_INTERNAL int64_t p2p_robust_pair_tile(int32_t rule);
+// K > 128: the median always runs the pair kernels (any K, padded), whose
+// tile is p2p_robust_pair_tile; the trimmed mean runs them or these LDS
+// kernels by the trim, on the same 64-coordinate tile.
 extern "C" P2P_INTERNAL int64_t p2p_robust_lds_tile(int32_t rule, int32_t k) {
-  (void)rule;
   (void)k;
-  return LdsLayout<4, 64>::TB;
+  static_assert(LdsLayout<4, 64>::TB == 64, "trimmed: pair and LDS kernels share the tile");
+  return rule == P2P_RULE_MEDIAN ? p2p_robust_pair_tile(rule) : LdsLayout<4, 64>::TB;
 }
 
 extern "C" P2P_INTERNAL int32_t p2p_robust_pair_fits(int32_t rule, int32_t k, int32_t trim_b);
@@ -666,11 +670,10 @@ extern "C" P2P_INTERNAL void p2p_robust_lds_launch(const float* const* peers, co
                                                    int32_t trim_b, int64_t n, float* w, float* out, float lr,
                                                    p2p_stream_t stream) {
   LdsArgs a{peers, segs, nseg, tiles, k, trim_b, n, w, out, lr, static_cast<hipStream_t>(stream)};
-  const bool med = rule == P2P_RULE_MEDIAN;
-  if (p2p_robust_pair_fits(rule, k, trim_b)) {
+  // the median fits the pair kernels at every K in 129..256 (its tile differs
+  // from these kernels': p2p_robust_lds_tile)
+  if (rule == P2P_RULE_MEDIAN || p2p_robust_pair_fits(rule, k, trim_b)) {
     p2p_robust_pair_launch(peers, segs, nseg, tiles, rule, k, trim_b, n, w, out, lr, stream);
-  } else if (med) {
-    if (segs) launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, true>(a); else launch_lds_g2_kernel<P2P_RULE_MEDIAN, 0, false>(a);
   } else {
     if (segs) launch_lds_g2_kernel<P2P_RULE_TRIMMED, 0, true>(a); else launch_lds_g2_kernel<P2P_RULE_TRIMMED, 0, false>(a);
   }

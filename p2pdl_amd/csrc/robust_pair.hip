@@ -39,7 +39,11 @@
 
 namespace p2p {
 
-constexpr int kPairTile = 64;  // coordinates per block, one lane each
+constexpr int kPairTile = 64;  // coordinates per wave pair, one lane each
+// Wave pairs per block: the median kernel runs two pairs on adjacent 64-
+// coordinate tiles, so each peer row is read 512 contiguous bytes per block
+// (two 256-B wave loads issued together) instead of 256.
+constexpr int kMedianPairs = 2;
 constexpr int kHalf = 128;     // peers per wave
 
 __device__ __forceinline__ float val(fk x) { return x.x; }
@@ -149,11 +153,11 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
 // two-set search (robust_nets.h).  Against two Batcher sorts of 128 and the
 // flip this issues 17% fewer VALU instructions per coordinate; the 16 KB
 // image leaves room for 3 blocks' worth of waves per SIMD pair.
-template <typename T, bool FLAGS = false, bool PAD = false>
+template <typename T, bool FLAGS = false, bool PAD = false, int NP = 1>
 __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im, int h, int lane,
                                              int __attribute__((address_space(3)))* flags = nullptr,
                                              const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0,
-                                             int K = 2 * kHalf, const Pads& pd = Pads{}) {
+                                             int K = 2 * kHalf, const Pads& pd = Pads{}, int pr = 0) {
   constexpr int Q = kHalf / 2;  // 64 keys per sorted list
   // FLAGS: each list's NaN test right before its sort, so sorting p overlaps
   // q's loads (a test of all 128 up front waited for every load: +3.5% time)
@@ -178,11 +182,11 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
   auto part = (uint32_t __attribute__((address_space(3)))*)(im + Q / 4 * 64);  // max(lo) of wave h at [64h + lane]
   part[h * 64 + lane] = raw(m);
   if constexpr (FLAGS) {
-    if (lane == 0) flags[h] = has_nan ? 1 : 0;
+    if (lane == 0) flags[2 * pr + h] = has_nan ? 1 : 0;
   }
   block_sync();  // 1: both max(lo)
-  if constexpr (FLAGS) {
-    if (uniform((flags[0] | flags[1]) != 0))
+  if constexpr (FLAGS) {  // block-wide: every pair of the block takes the same path (same barriers)
+    if (uniform((flags[0] | flags[1] | (NP > 1 ? flags[2] | flags[3] : 0)) != 0))
       return pair_keys<P2P_RULE_MEDIAN, PAD>(P, c0, lane_off, im, h, lane, K, pd.kr, pd.lo, pd.m);
   }
   const T mo = from_raw<T>(part[(1 - h) * 64 + lane]);
@@ -366,7 +370,8 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
   K = __builtin_amdgcn_readfirstlane(K);
   uint32_t v[kHalf];
   load_half<PAD, true>(v, P, c0, lane_off, h, K, pd.lo);
-  if constexpr (RULE == P2P_RULE_MEDIAN) return median_pair<uint32_t, false, PAD>(v, im, h, lane, nullptr, P, c0, lane_off, K, pd);
+  if constexpr (RULE == P2P_RULE_MEDIAN)
+    return median_pair<uint32_t, false, PAD>(v, im, h, lane, nullptr, P, c0, lane_off, K, pd);
   else return pair_body<RULE, kx, false, PAD>(v, im, h, lane, nullptr, P, c0, lane_off, K, pd);  // kx: max as a ^ b ^ min
 }
 
@@ -374,30 +379,37 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
 // 2^30 floats): the tile start rides in the 32-bit lane offset and each peer
 // row's pointer is the scalar base as loaded -- no 64-bit scalar add per load
 // (256 SALU instructions per wave and tile).
-template <int RULE, bool SEGS, bool SMALL, bool PAD>
+// NP wave pairs per block: pair pr takes coordinates 64 pr .. 64 pr + 63 of
+// the block's tile (its own LDS image, im already offset).
+template <int RULE, bool SEGS, bool SMALL, bool PAD, int NP = 1>
 __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers, const Seg* __restrict__ segs,
                                           int nseg, int64_t n, float* w, float* out, float lr, Img im,
                                           int __attribute__((address_space(3)))* flags, int64_t t, int K, int trim_b) {
-  const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 6));
+  const int h = __builtin_amdgcn_readfirstlane(static_cast<int>(NP == 1 ? tid_x() >> 6 : (tid_x() >> 6) & 1));
+  const int pr = NP == 1 ? 0 : __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 7));
   const int lane = tid_x() & 63;
   const float* const* P = peers;
   float* W = w;
   float* O = out;
-  int64_t N = n, c0 = t * kPairTile;
+  int64_t N = n, c0 = t * (kPairTile * NP) + pr * kPairTile;
   if constexpr (SEGS) {
     const Seg s = load_segment(segs, nseg, t);
     P = s.peers;
     W = s.w;
     O = s.out;
     N = s.n;
-    c0 = (t - s.tile_begin) * kPairTile;
+    c0 = (t - s.tile_begin) * (kPairTile * NP) + pr * kPairTile;
   }
   const int64_t i = c0 + lane;
-  // Dead lanes of a ragged tail re-read the last element.
+  // Dead lanes of a ragged tail re-read the last element; with NP > 1 a
+  // whole wave pair can lie past the end (it still joins the block's
+  // barriers), so its row base is clamped too: 0 <= lane_off < 256 whenever
+  // the base carries the tile start.
   // row base offset (SMALL: 0, the whole offset rides per lane; never for
   // PAD, whose pad rows are one tile wide)
-  const int64_t cb = SMALL && !PAD ? 0 : c0;
-  const uint32_t lane_off = static_cast<uint32_t>((i < N ? i : N - 1) - cb) * 4u;
+  const int64_t ic = i < N ? i : N - 1;
+  const int64_t cb = SMALL && !PAD ? 0 : (c0 < N ? c0 : N - 1);
+  const uint32_t lane_off = static_cast<uint32_t>(ic - cb) * 4u;
   Pads pd;
   if constexpr (PAD) {
     pd.kr = h == 0 ? kHalf : K - kHalf;
@@ -409,7 +421,8 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
   // One domain per block: the float network unless either half holds a NaN
   // (flags swapped at the first barrier, no barrier of their own).
   float agg;
-  if constexpr (RULE == P2P_RULE_MEDIAN) agg = median_pair<fk, true, PAD>(v, im, h, lane, flags, P, cb, lane_off, K, pd);
+  if constexpr (RULE == P2P_RULE_MEDIAN)
+    agg = median_pair<fk, true, PAD, NP>(v, im, h, lane, flags, P, cb, lane_off, K, pd, pr);
   else agg = pair_body<RULE, fk, true, PAD>(v, im, h, lane, flags, P, cb, lane_off, K, pd);
   if (h == 0 && i < N) {  // wave 0 holds the aggregate
     if (O) stg(O + i, agg);
@@ -431,23 +444,32 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void r
                                                 (int __attribute__((address_space(3)))*)nan_flag, t, K, trim_b);
 }
 
-// Median: 16 KB image (B's kept half) + both max(lo) (512 B), 3 waves per
-// SIMD (<= 168 VGPRs).
+// Median: per wave pair a 16 KB image (B's kept half) + both max(lo)
+// (512 B); kMedianPairs pairs per block, 3 waves per SIMD (<= 168 VGPRs).
 template <bool SEGS, bool SMALL = false, bool PAD = false>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void robust_median_pair_kernel(
-    const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n, float* w,
-    float* out, float lr, int64_t ntiles, unsigned gx, int K, int trim_b) {
-  __shared__ u32x4 img_raw[kHalf / 8 * 64 + 32];
-  __shared__ int nan_flag[2];
+__global__ __launch_bounds__(128 * kMedianPairs) __attribute__((amdgpu_waves_per_eu(3))) void
+robust_median_pair_kernel(const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n,
+                          float* w, float* out, float lr, int64_t ntiles, unsigned gx, int K, int trim_b) {
+  constexpr int kImg = kHalf / 8 * 64 + 32;
+  __shared__ u32x4 img_raw[kImg * kMedianPairs];
+  __shared__ int nan_flag[2 * kMedianPairs];
   const int64_t t = tile_id(gx);
   if (t >= ntiles) return;  // block-uniform
-  pair_tile<P2P_RULE_MEDIAN, SEGS, SMALL, PAD>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
-                                               (int __attribute__((address_space(3)))*)nan_flag, t, K, trim_b);
+  const int pr = kMedianPairs == 1 ? 0 : __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 7));
+  pair_tile<P2P_RULE_MEDIAN, SEGS, SMALL, PAD, kMedianPairs>(peers, segs, nseg, n, w, out, lr,
+                                                             (Img)img_raw + pr * kImg,
+                                                             (int __attribute__((address_space(3)))*)nan_flag, t,
+                                                             K, trim_b);
 }
 
 }  // namespace p2p
 
 using namespace p2p;
+
+// Coordinates per block tile of the pair kernels.
+extern "C" P2P_INTERNAL int64_t p2p_robust_pair_tile(int32_t rule) {
+  return rule == P2P_RULE_MEDIAN ? kPairTile * kMedianPairs : kPairTile;
+}
 
 // Whether the pair kernels take (rule, K, b): K = 256 with the median or
 // b = 51 as built; K in 129..255 (or another b) padded to 256 when the pads
@@ -468,10 +490,11 @@ extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, c
                                                     int32_t trim_b, int64_t n, float* w, float* out, float lr,
                                                     p2p_stream_t stream) {
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  const int64_t ntiles = segs ? tiles : ceil_div(n, kPairTile);
-  const TileGrid tg = tile_grid(ntiles);  // 2 x 64 lanes per 64 coordinates: 1-D, n > 2^31 would wrap
+  const int np = rule == P2P_RULE_MEDIAN ? kMedianPairs : 1;  // p2p_robust_pair_tile
+  const int64_t ntiles = segs ? tiles : ceil_div(n, kPairTile * np);
+  const TileGrid tg = tile_grid(ntiles, 128 * np);  // 2 x 64 lanes per 64 coordinates: 1-D, n > 2^31 would wrap
   if (tg.gx == 0) return;
-  const dim3 g(tg.gx, tg.gy), b(2 * 64);
+  const dim3 g(tg.gx, tg.gy), b(2 * 64 * np);
   const bool pad = !(k == 2 * kHalf && (rule == P2P_RULE_MEDIAN || trim_b == 51));
   const bool small = !segs && n <= (int64_t(1) << 30);
 #define P2P_PAIR_ARGS g, b, 0, st, peers, segs, nseg, n, w, out, lr, ntiles, tg.gx, k, trim_b

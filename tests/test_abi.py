@@ -36,7 +36,10 @@ def test_abi_version_and_argument_errors_without_gpu():
     # tile sizes are a pure function of (rule, k): no process-wide layout state
     assert L.p2p_tile_elems(0, 3) == 4096 and L.p2p_tile_elems(0, 256) == 4096
     assert L.p2p_tile_elems(1, 64) == 128 and L.p2p_tile_elems(1, 128) == 128
-    assert L.p2p_tile_elems(1, 129) == 64 and L.p2p_tile_elems(2, 200) == 64 and L.p2p_tile_elems(1, 256) == 64
+    # K > 128: the median pair kernel runs two wave pairs (128 coordinates)
+    # per block; the trimmed mean's pair and LDS kernels share 64
+    assert L.p2p_tile_elems(1, 129) == 128 and L.p2p_tile_elems(1, 256) == 128
+    assert L.p2p_tile_elems(2, 200) == 64 and L.p2p_tile_elems(2, 256) == 64
     # argument validation happens before any HIP call
     assert L.p2p_fedavg_apply_f32(None, 3, 10, None, 0.1, None) == N.lib().p2p_aggregate_f32(
         None, 1, 1, 0, 0, 0.1, None, None, None) == -1

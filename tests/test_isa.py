@@ -78,9 +78,11 @@ def test_float_network_always_behind_the_nan_test(funcs):
         # per instruction, into a pair that one compare tests; the padded
         # kernels' slots that may hold +-inf pad rows fold 2 keys per
         # v_maximum3_f32 instead; plain compares test 2 keys each -- either way
-        # 4 * pk + 2 * mx + 2 * cmps keys are covered
+        # 4 * pk + 2 * mx + 2 * cmps keys are covered (each chain's compare
+        # counts the two extra keys its first instruction folds); the loads
+        # include one that is not a key (the w read of the apply)
         loads = sum(v for k, v in c.items() if k.startswith("global_load") and "lds" not in k)
-        assert cmps > 0 and 4 * pk + 2 * mx + 2 * cmps >= loads > 0, (name, cmps, pk, mx, loads)
+        assert cmps > 0 and 4 * pk + 2 * mx + 2 * cmps >= loads - 1 > 0, (name, cmps, pk, mx, loads)
         checked += 1
     assert checked >= 6
 
