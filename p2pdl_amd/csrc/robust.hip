@@ -105,13 +105,13 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
   // load); the asm keeps LLVM from re-associating the tile start into it.
   uint32_t v[KP];
   const int lo = PAD ? pad_lo(KP, RULE, K, trim_b) : 0;
-  const uint64_t prow = reinterpret_cast<uint64_t>(pad_row(KEYS, false));  // the top row is 512 B on
+  const uint64_t prow = reinterpret_cast<uint64_t>(pad_row(KEYS, false));  // the top row follows it
 #pragma unroll
   for (int j = 0; j < KP; ++j) {
     const bool real = (MODE != 0 && !PAD) || (PAD && 2 * j < KP) || (j < K);  // PAD: K > KP / 2
     uint64_t row = reinterpret_cast<uint64_t>(table_at(peers, PAD ? min(j, K - 1) : real ? j : 0) + c0);
     // PAD: a pad slot reads its pad row (no c0: the row is one tile wide)
-    if (PAD && !real) row = prow + (j - K >= lo ? 512u : 0u);
+    if (PAD && !real) row = prow + (j - K >= lo ? kPadRowBytes : 0u);
     asm("" : "+s"(row));
     const P2P_GLOBAL float* src =
         reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off);
@@ -263,7 +263,7 @@ struct RobustArgs {
 template <int KP, int RULE, int MODE, bool PAD = false>
 static void launch_one(const RobustArgs& a) {
   const int64_t tiles = a.segs ? a.tiles : ceil_div(a.n, kRobustTile);
-  const TileGrid g = tile_grid(tiles);
+  const TileGrid g = tile_grid(tiles, kRobustTile);
   if (g.gx == 0) return;
   if (a.segs) {
     hipLaunchKernelGGL((robust_segments_kernel<KP, RULE, MODE, PAD>), dim3(g.gx, g.gy), dim3(kRobustTile), 0, a.stream,

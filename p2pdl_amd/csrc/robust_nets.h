@@ -125,15 +125,18 @@ __device__ __forceinline__ void ce(fx& a, fx& b) {
   if constexpr (ASC) { a.x = lo; b.x = hi; } else { a.x = hi; b.x = lo; }
 }
 // Pad rows of the padded robust kernels (K below the network's size): a pad
-// slot loads lane l's word from one of these 128-word rows instead of a peer
+// slot loads lane l's word from one of these 256-word rows instead of a peer
 // row -- L1/L2-resident, no HBM traffic, no VALU select -- so the network
 // sees -inf / +inf (float path) or the bottom / top key (key path: float bits
 // 0xFFFFFFFF and 0x7FFFFFFF, which f2key maps to 0 and ~0).
 #define P2P_R4(x) x, x, x, x
 #define P2P_R16(x) P2P_R4(x), P2P_R4(x), P2P_R4(x), P2P_R4(x)
 #define P2P_R128(x) P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x), P2P_R16(x)
-__device__ static const uint32_t kPadRows[4][128] = {{P2P_R128(0xFF800000u)}, {P2P_R128(0x7F800000u)},
-                                                     {P2P_R128(0xFFFFFFFFu)}, {P2P_R128(0x7FFFFFFFu)}};
+#define P2P_R256(x) P2P_R128(x), P2P_R128(x)
+constexpr unsigned kPadRowBytes = 1024;  // one word per lane of a 256-lane block
+__device__ static const uint32_t kPadRows[4][kPadRowBytes / 4] = {
+    {P2P_R256(0xFF800000u)}, {P2P_R256(0x7F800000u)}, {P2P_R256(0xFFFFFFFFu)}, {P2P_R256(0x7FFFFFFFu)}};
+#undef P2P_R256
 #undef P2P_R128
 #undef P2P_R16
 #undef P2P_R4

@@ -337,12 +337,12 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
 template <bool PAD = false, bool KEYS = false>
 __device__ __forceinline__ void load_half(uint32_t (&v)[kHalf], const float* const* P, int64_t c0,
                                           uint32_t lane_off, int h, int K = 2 * kHalf, int lo = 0) {
-  const uint64_t prow = reinterpret_cast<uint64_t>(pad_row(KEYS, false));  // the top row is 512 B on
+  const uint64_t prow = reinterpret_cast<uint64_t>(pad_row(KEYS, false));  // the top row follows it
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) {
     const int slot = h * kHalf + j;
     uint64_t row = reinterpret_cast<uint64_t>(table_at(P, PAD ? min(slot, K - 1) : slot) + c0);
-    if (PAD && slot >= K) row = prow + (slot - K >= lo ? 512u : 0u);
+    if (PAD && slot >= K) row = prow + (slot - K >= lo ? kPadRowBytes : 0u);
     asm("" : "+s"(row));
     const P2P_GLOBAL float* src =
         reinterpret_cast<const P2P_GLOBAL float*>(reinterpret_cast<const P2P_GLOBAL char*>(row) + lane_off);
