@@ -125,7 +125,6 @@ __device__ __forceinline__ void pin(const T (&x)[N]) {
 // row (robust_nets.h pad_row: the row is one tile wide, so the PAD kernels
 // keep the tile start in the row base, not in the lane offset).
 struct Pads {
-  int kr = kHalf;  // real slots in this wave
   int lo = 0;      // low pads
   int m = 2 * kHalf - 2 * 51;  // trimmed: kept ranks
 };
@@ -141,7 +140,7 @@ __device__ __forceinline__ uint64_t list_nan_mask(const uint32_t* v) {
 // number of block barriers.
 template <int RULE, bool PAD>
 __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int64_t c0, uint32_t lane_off, Img im,
-                                                     int h, int lane, int K, int kr, int lo, int m);
+                                                     int h, int lane, int K, int lo, int m);
 
 // MEDIAN (rank 127 of 256) without sorting the halves: wave h sorts its
 // peers as two lists of 64 (p = peers 128h..128h+63, q = the next 64) and
@@ -187,7 +186,7 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
   block_sync();  // 1: both max(lo)
   if constexpr (FLAGS) {  // block-wide: every pair of the block takes the same path (same barriers)
     if (uniform((flags[0] | flags[1] | (NP > 1 ? flags[2] | flags[3] : 0)) != 0))
-      return pair_keys<P2P_RULE_MEDIAN, PAD>(P, c0, lane_off, im, h, lane, K, pd.kr, pd.lo, pd.m);
+      return pair_keys<P2P_RULE_MEDIAN, PAD>(P, c0, lane_off, im, h, lane, K, pd.lo, pd.m);
   }
   const T mo = from_raw<T>(part[(1 - h) * 64 + lane]);
   const bool d = h == 0 ? le(m, mo) : le(mo, m);  // max(A_lo) <= max(B_lo): A_hi u B_lo
@@ -255,7 +254,7 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   block_sync();  // 1: both parities in the image
   if constexpr (FLAGS) {
     if (uniform((flags[0] | flags[1]) != 0))
-      return pair_keys<RULE, PAD>(P, c0, lane_off, im, h, lane, K, pd.kr, pd.lo, pd.m);
+      return pair_keys<RULE, PAD>(P, c0, lane_off, im, h, lane, K, pd.lo, pd.m);
   }
   {
     constexpr int b = (2 * kHalf * 2) / 10;  // 51: ranks b..2*kHalf-b-1 = 51..204 kept
@@ -358,13 +357,12 @@ __device__ __forceinline__ void load_half(uint32_t (&v)[kHalf], const float* con
 // live for this one (inlined, the two paths took 320-390 VGPRs).
 template <int RULE, bool PAD>
 __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int64_t c0, uint32_t lane_off, Img im,
-                                                     int h, int lane, int K, int kr, int lo, int m) {
+                                                     int h, int lane, int K, int lo, int m) {
   // arguments arrive in VGPRs: make the wave-uniform ones scalar again
   P = reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(P)));
   c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(c0)));
   h = __builtin_amdgcn_readfirstlane(h);
   Pads pd;
-  pd.kr = __builtin_amdgcn_readfirstlane(kr);
   pd.lo = __builtin_amdgcn_readfirstlane(lo);
   pd.m = __builtin_amdgcn_readfirstlane(m);
   K = __builtin_amdgcn_readfirstlane(K);
@@ -412,7 +410,6 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
   const uint32_t lane_off = static_cast<uint32_t>(ic - cb) * 4u;
   Pads pd;
   if constexpr (PAD) {
-    pd.kr = h == 0 ? kHalf : K - kHalf;
     pd.lo = RULE == P2P_RULE_MEDIAN ? (2 * kHalf - 1) / 2 - (K - 1) / 2 : (2 * kHalf * 2) / 10 - trim_b;
     pd.m = K - 2 * trim_b;
   }
