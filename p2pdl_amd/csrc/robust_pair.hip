@@ -44,6 +44,7 @@ constexpr int kPairTile = 64;  // coordinates per wave pair, one lane each
 // coordinate tiles, so each peer row is read 512 contiguous bytes per block
 // (two 256-B wave loads issued together) instead of 256.
 constexpr int kMedianPairs = 2;
+constexpr int kTrimPairs = 1;  // the trimmed mean's pair and LDS kernels share the 64-coordinate tile
 constexpr int kHalf = 128;     // peers per wave
 
 __device__ __forceinline__ float val(fk x) { return x.x; }
@@ -210,11 +211,11 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
 // FLAGS (float path): the two waves swap "my half holds a NaN" at barrier 1,
 // beside the hand-off; a block that finds one re-runs the tile on the key
 // network (pair_keys) -- the float sort of a NaN half is discarded.
-template <int RULE, typename T, bool FLAGS = false, bool PAD = false>
+template <int RULE, typename T, bool FLAGS = false, bool PAD = false, int NP = 1>
 __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, int h, int lane,
                                            int __attribute__((address_space(3)))* flags = nullptr,
                                            const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0,
-                                           int K = 2 * kHalf, const Pads& pd = Pads{}) {
+                                           int K = 2 * kHalf, const Pads& pd = Pads{}, int pr = 0) {
   T x[kHalf];
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) x[j] = from_bits<T>(v[j]);
@@ -249,11 +250,11 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
     asm volatile("; parity hand-off, wave 1" ::: "memory");
   }
   if constexpr (FLAGS) {
-    if (lane == 0) flags[h] = has_nan ? 1 : 0;
+    if (lane == 0) flags[2 * pr + h] = has_nan ? 1 : 0;
   }
   block_sync();  // 1: both parities in the image
-  if constexpr (FLAGS) {
-    if (uniform((flags[0] | flags[1]) != 0))
+  if constexpr (FLAGS) {  // block-wide (same barriers for every pair)
+    if (uniform((flags[0] | flags[1] | (NP > 1 ? flags[2] | flags[3] : 0)) != 0))
       return pair_keys<RULE, PAD>(P, c0, lane_off, im, h, lane, K, pd.lo, pd.m);
   }
   {
@@ -420,7 +421,7 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
   float agg;
   if constexpr (RULE == P2P_RULE_MEDIAN)
     agg = median_pair<fk, true, PAD, NP>(v, im, h, lane, flags, P, cb, lane_off, K, pd, pr);
-  else agg = pair_body<RULE, fk, true, PAD>(v, im, h, lane, flags, P, cb, lane_off, K, pd);
+  else agg = pair_body<RULE, fk, true, PAD, NP>(v, im, h, lane, flags, P, cb, lane_off, K, pd, pr);
   if (h == 0 && i < N) {  // wave 0 holds the aggregate
     if (O) stg(O + i, agg);
     if (W) stg(W + i, apply_lr(ldg(W + i), lr, agg));
@@ -430,14 +431,16 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
 // Trimmed mean: two 16 KB parity regions + the partial sums (256 B), 2 waves
 // per SIMD.
 template <bool SEGS, bool SMALL = false, bool PAD = false>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(
+__global__ __launch_bounds__(128 * kTrimPairs) __attribute__((amdgpu_waves_per_eu(2))) void robust_pair_kernel(
     const float* const* __restrict__ peers, const Seg* __restrict__ segs, int nseg, int64_t n, float* w,
     float* out, float lr, int64_t ntiles, unsigned gx, int K, int trim_b) {
-  __shared__ u32x4 img_raw[kHalf / 4 * 64 + 16];
-  __shared__ int nan_flag[2];
+  constexpr int kImg = kHalf / 4 * 64 + 16;
+  __shared__ u32x4 img_raw[kImg * kTrimPairs];
+  __shared__ int nan_flag[2 * kTrimPairs];
   const int64_t t = tile_id(gx);
   if (t >= ntiles) return;  // block-uniform
-  pair_tile<P2P_RULE_TRIMMED, SEGS, SMALL, PAD>(peers, segs, nseg, n, w, out, lr, (Img)img_raw,
+  const int pr = kTrimPairs == 1 ? 0 : __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 7));
+  pair_tile<P2P_RULE_TRIMMED, SEGS, SMALL, PAD, kTrimPairs>(peers, segs, nseg, n, w, out, lr, (Img)img_raw + pr * kImg,
                                                 (int __attribute__((address_space(3)))*)nan_flag, t, K, trim_b);
 }
 
@@ -465,7 +468,7 @@ using namespace p2p;
 
 // Coordinates per block tile of the pair kernels.
 extern "C" P2P_INTERNAL int64_t p2p_robust_pair_tile(int32_t rule) {
-  return rule == P2P_RULE_MEDIAN ? kPairTile * kMedianPairs : kPairTile;
+  return kPairTile * (rule == P2P_RULE_MEDIAN ? kMedianPairs : kTrimPairs);
 }
 
 // Whether the pair kernels take (rule, K, b): K = 256 with the median or
@@ -487,7 +490,7 @@ extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, c
                                                     int32_t trim_b, int64_t n, float* w, float* out, float lr,
                                                     p2p_stream_t stream) {
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  const int np = rule == P2P_RULE_MEDIAN ? kMedianPairs : 1;  // p2p_robust_pair_tile
+  const int np = rule == P2P_RULE_MEDIAN ? kMedianPairs : kTrimPairs;  // p2p_robust_pair_tile
   const int64_t ntiles = segs ? tiles : ceil_div(n, kPairTile * np);
   const TileGrid tg = tile_grid(ntiles, 128 * np);  // 2 x 64 lanes per 64 coordinates: 1-D, n > 2^31 would wrap
   if (tg.gx == 0) return;
