@@ -965,7 +965,9 @@ def run_inbox_workload(args, K, n, seed, dev):
         return [inbox.digest(k) for k in range(len(msgs))]
 
     t_pin, t_pin_dig = timed(ours_pinned), timed(ours_pinned_digest)
-    t_ours, t_ref = timed(ours), timed(reference)
+    # the broadcast's own path: the parts it sends (node.envelope.envelope_parts);
+    # the joined bytes object beside it
+    t_joined, t_ref, t_ours = timed(ours), timed(reference), timed(ours_parts)
     t_dig, t_seq, t_ref_dig = timed(ours_digest), timed(land_then_hash), timed(reference_echo)
     n = sum(_numel(s) for _, s in shapes)
     nbytes = K * n * 4
@@ -1115,14 +1117,17 @@ def run_broadcast_workload(args, seed, dev):
     """Global-model serialization before the broadcast (SURVEY §8(f) row 4;
     reference aggregator/aggregation.py:66-70): the tester pickles its
     ResNet-18-sized state_dict into the 'global_model_update' envelope.  The
-    reference pickles the CUDA state_dict, so torch copies every tensor to
-    the host separately inside pickle.dumps; the product brings all fp32
-    tensors over in ONE transfer into a reused pinned buffer
-    (aggregation._host_state_dict) and pickles host views.  value = model
-    bytes serialized per second (device-to-host + pickle)."""
+    reference pickles the CUDA state_dict: torch copies every tensor to the
+    host, into a BytesIO, out of it and into the pickle.  The product
+    (node/envelope.py) DMAs each fp32 tensor into a pinned slot laid out as
+    torch's storage blob and pickles the slots in-band (protocol 5): the
+    joined envelope costs one copy of the weights; the parts the broadcast
+    sends (envelope_parts) none.  value = model bytes serialized per second
+    into the parts the broadcast sends (device-to-host + pickle);
+    joined_ms: the same into one bytes object."""
     import pickle
 
-    from p2pdl_amd.aggregator import aggregation as agg
+    from p2pdl_amd.node import envelope as env
 
     shapes = resnet18_param_shapes()
     model = torch.nn.Module()
@@ -1136,7 +1141,11 @@ def run_broadcast_workload(args, seed, dev):
         return pickle.dumps({"type": "global_model_update", "model": state, "addr": "127.0.0.1", "port": 1})
 
     def ours():
-        return envelope(agg._host_state_dict(model.state_dict()))
+        return env.global_model_envelope(model.state_dict(), "127.0.0.1", 1)
+
+    def ours_parts():
+        with env.LOCK:
+            return sum(p.nbytes for p in env.envelope_parts(model.state_dict(), "127.0.0.1", 1))
 
     def reference():
         return envelope(model.state_dict())
@@ -1156,7 +1165,9 @@ def run_broadcast_workload(args, seed, dev):
             fn()
         return (time.perf_counter() - t0) / args.steps
 
-    t_ours, t_ref = timed(ours), timed(reference)
+    # the broadcast's own path: the parts it sends (node.envelope.envelope_parts);
+    # the joined bytes object beside it
+    t_joined, t_ref, t_ours = timed(ours), timed(reference), timed(ours_parts)
     nbytes = 4 * sum(_numel(s) for _, s in shapes)
     del model
     torch.cuda.empty_cache()
@@ -1167,6 +1178,8 @@ def run_broadcast_workload(args, seed, dev):
         "config": {"workload": f"broadcast: the global_model_update envelope of a {len(shapes)}-tensor state_dict "
                                f"({nbytes / 4:,.0f} params) pickled from the GPU model (SURVEY §8(f) row 4)",
                    "reference_ms": round(t_ref * 1e3, 3), "speedup_vs_reference": round(t_ref / t_ours, 2),
+                   "joined_ms": round(t_joined * 1e3, 3),
+                   "speedup_joined_vs_reference": round(t_ref / t_joined, 2),
                    "parallelism": "single GPU, device-to-host"},
         "roofline": {"bound": "pcie (device-to-host) + host pickle", "achieved": round(nbytes / t_ours / 1e9, 2),
                      "peak": 63.0, "unit": "GB/s", "frac": round(nbytes / t_ours / 1e9 / 63.0, 4), "traffic": None},
@@ -1215,7 +1228,7 @@ def compact_sub(rec: dict) -> dict:
             out["traffic_x"] = round(tr / alg, 5)
     cfg = rec.get("config") or {}
     for k in ("reference_ms", "staging_ms", "pinned_digest_overlapped_ms", "with_digest", "hashes_product",
-              "speedup_vs_reference"):
+              "speedup_vs_reference", "joined_ms"):
         if k in cfg:
             v = cfg[k]
             out[k] = {a: b for a, b in v.items() if a != "what"} if isinstance(v, dict) else v

@@ -32,6 +32,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..node import envelope
 from ..node.inbox import LandedUpdate
 from ..utils.waiting import wait_for_models
 from .model_state import model_state
@@ -250,59 +251,24 @@ def _mark_rows_consumed(received) -> None:
         inbox.slab_consumed()
 
 
-_PINNED = {}  # (device, numel) -> pinned host staging buffer, reused across rounds
-
-
-def _host_state_dict(state):
-    """state_dict with every tensor on the host, fp32 GPU tensors brought over
-    in ONE device-to-host copy: the reference pickles
-    the CUDA state_dict, and torch then copies each tensor to the host
-    separately while pickling (aggregation.py:70).  Each host tensor owns just
-    its own bytes (a numpy slice), so the pickle carries no more than the
-    reference's."""
-    gpu = [(k, t) for k, t in state.items() if t.is_cuda and t.dtype == torch.float32]
-    host = {}
-    if gpu:
-        dev = gpu[0][1].device
-        total = sum(t.numel() for _, t in gpu)
-        buf = _PINNED.get((dev, total))
-        if buf is None:
-            buf = torch.empty(total, dtype=torch.float32, pin_memory=True)
-            _PINNED.clear()
-            _PINNED[(dev, total)] = buf
-        with torch.cuda.device(dev):
-            flat = torch.cat([t.detach().reshape(-1) for _, t in gpu])
-            buf.copy_(flat, non_blocking=True)
-            torch.cuda.current_stream(dev).synchronize()
-        arr = buf.numpy()
-        off = 0
-        for k, t in gpu:
-            n = t.numel()
-            host[k] = torch.from_numpy(arr[off:off + n]).view(t.shape)
-            off += n
-    out = type(state)()
-    for k, t in state.items():
-        out[k] = host[k] if k in host else t.detach().cpu()
-    return out
-
-
 def broadcast_global_model_update(self):
     """Behaviour of reference aggregation.py:66-77 (networking is out of
     scope): pickle the state_dict, one TCP connection per neighbour, 4-byte
-    big-endian length prefix.  The state is pickled from host copies made with
-    one device-to-host transfer; receivers see the same keys and values
+    big-endian length prefix.  The envelope is node.envelope's: each fp32
+    weight lands by DMA in a pinned slot laid out as torch's storage blob and
+    the socket sends it from there; receivers see the same keys and values
     (the reference receiver only calls load_state_dict, node/node.py:242-244).
     A message over 2**32-1 bytes cannot be framed by the 4-byte prefix: the
     reference fails inside to_bytes; this raises a clear error first."""
-    model_state = _host_state_dict(self.model.state_dict())
-    data = pickle.dumps({"type": "global_model_update", "model": model_state,
-                         "addr": self.addr, "port": self.port})
-    msg_len = len(data)
-    if msg_len > 0xFFFFFFFF:
-        raise OverflowError(f"global model message of {msg_len} bytes exceeds the 4-byte length prefix")
-    for neighbor in self.neighbors:
-        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-            s.connect((neighbor.addr, neighbor.port))
-            s.sendall(msg_len.to_bytes(4, byteorder="big"))
-            s.sendall(data)
-            logging.debug(f"Broadcasted global model update to {neighbor.addr}:{neighbor.port}")
+    with envelope.LOCK:  # the parts alias the envelope's pinned buffer until sent
+        parts = envelope.envelope_parts(self.model.state_dict(), self.addr, self.port)
+        msg_len = sum(p.nbytes for p in parts)
+        if msg_len > 0xFFFFFFFF:
+            raise OverflowError(f"global model message of {msg_len} bytes exceeds the 4-byte length prefix")
+        for neighbor in self.neighbors:
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+                s.connect((neighbor.addr, neighbor.port))
+                s.sendall(msg_len.to_bytes(4, byteorder="big"))
+                for p in parts:  # the weights straight from the DMA target
+                    s.sendall(p)
+                logging.debug(f"Broadcasted global model update to {neighbor.addr}:{neighbor.port}")

@@ -1,0 +1,182 @@
+"""The global model's broadcast envelope, serialized with one copy of the
+weights (reference aggregator/aggregation.py:66-70).
+
+The reference pickles ``{"type": "global_model_update", "model":
+state_dict, "addr", "port"}`` with the CUDA tensors inside.  torch pickles a
+tensor as ``torch._utils._rebuild_tensor_v2(storage, offset, size, stride,
+requires_grad, OrderedDict())`` and each storage as
+``torch.storage._load_from_bytes(blob)``, the blob being torch's legacy
+``torch.save`` stream of that storage: four small pickles (magic number,
+protocol version 1001, sys_info, a persistent-id reference), the storage key
+list, an 8-byte element count and the raw bytes.  Building it, torch copies
+each storage to the host, into a BytesIO, out of it, and into the pickle:
+three copies of every weight after the device-to-host one.
+
+Here the fp32 weights land by device-to-host DMA straight into a pinned
+buffer laid out as those blobs -- each blob's header and count written once
+when the buffer is made (they depend on the tensor sizes only) -- and the
+envelope is pickled with protocol 5, each blob an in-band ``PickleBuffer``
+over its slot, which the pickler hands to its writer uncopied: the
+broadcast sends the weights straight from the DMA target
+(``envelope_parts``), or one join makes the bytes (``global_model_envelope``).  The
+receiver's ``pickle.loads`` (reference node/node.py:112) and
+``p2pdl_amd.node.inbox.ZeroCopyParser`` read it like torch's own pickle
+(``tests/test_envelope.py`` checks the blobs against ``torch.save`` byte for
+byte and the envelope against ``pickle.loads``).
+"""
+from __future__ import annotations
+
+import collections
+import io
+import pickle
+import threading
+
+import numpy as np
+import torch
+
+__all__ = ["LOCK", "envelope_parts", "global_model_envelope", "legacy_storage_header"]
+
+# torch.serialization's legacy stream: magic number, protocol version, sys_info
+_MAGIC = 0x1950A86A20F9469CFC6C
+_PROTOCOL_VERSION = 1001
+_SYS_INFO = {"protocol_version": _PROTOCOL_VERSION, "little_endian": True,
+             "type_sizes": {"short": 2, "int": 4, "long": 4}}
+
+
+class _StorageRef:
+    """Stands for the storage in the header's persistent-id pickle."""
+
+
+def legacy_storage_header(numel: int, key: str) -> bytes:
+    """The bytes torch's legacy ``torch.save`` of a float32 storage of
+    ``numel`` elements writes before the raw data: the four header pickles
+    (protocol 2, as torch writes them), the key list and the 8-byte count."""
+    f = io.BytesIO()
+    pickle.dump(_MAGIC, f, protocol=2)
+    pickle.dump(_PROTOCOL_VERSION, f, protocol=2)
+    pickle.dump(_SYS_INFO, f, protocol=2)
+    ref = _StorageRef()
+
+    class _P(pickle.Pickler):
+        def persistent_id(self, obj):
+            if obj is ref:
+                return ("storage", torch.FloatStorage, key, "cpu", numel, None)
+            return None
+
+    _P(f, protocol=2).dump(ref)
+    pickle.dump([key], f, protocol=2)
+    f.write(int(numel).to_bytes(8, "little"))
+    return f.getvalue()
+
+
+class _Blob:
+    """Pickles as torch.storage._load_from_bytes(<the slot's bytes>)."""
+    __slots__ = ("mv",)
+
+    def __init__(self, mv):
+        self.mv = mv
+
+    def __reduce__(self):
+        return (torch.storage._load_from_bytes, (pickle.PickleBuffer(self.mv),))
+
+
+class _Tensor:
+    """Pickles as torch._utils._rebuild_tensor_v2 over a _Blob, as torch
+    pickles a contiguous CPU tensor."""
+    __slots__ = ("blob", "size", "stride")
+
+    def __init__(self, blob, size, stride):
+        self.blob, self.size, self.stride = blob, size, stride
+
+    def __reduce__(self):
+        return (torch._utils._rebuild_tensor_v2,
+                (self.blob, 0, self.size, self.stride, False, collections.OrderedDict()))
+
+
+class _Layout:
+    """One pinned buffer of legacy blobs for a fixed list of fp32 sizes."""
+
+    def __init__(self, numels, pin: bool):
+        heads = [legacy_storage_header(n, str(i)) for i, n in enumerate(numels)]
+        self.spans = []  # (blob start, payload start, blob end) per tensor
+        off = 0
+        for h, n in zip(heads, numels):
+            self.spans.append((off, off + len(h), off + len(h) + 4 * n))
+            off += len(h) + 4 * n
+        self.buf = torch.empty(max(off, 1), dtype=torch.uint8, pin_memory=pin)  # DMA target for GPU weights
+        arr = self.buf.numpy()
+        for h, (a, p, _) in zip(heads, self.spans):
+            arr[a:p] = np.frombuffer(h, dtype=np.uint8)
+        self.mv = memoryview(arr).toreadonly()
+
+
+_LAYOUTS = {}
+LOCK = threading.RLock()  # held while envelope parts (which alias the pinned buffer) are in use
+
+
+class _Parts:
+    """The pickler's output as the buffers it hands over: small frames as
+    bytes, each weight blob as a view of its pinned slot (no copy)."""
+
+    def __init__(self):
+        self.parts = []
+        self.nbytes = 0
+
+    def write(self, b):
+        m = memoryview(b)
+        self.parts.append(m)
+        self.nbytes += m.nbytes
+        return m.nbytes
+
+
+def envelope_parts(state, addr, port):
+    """The global_model_update envelope as a list of buffers whose
+    concatenation is its pickle (protocol 5): every contiguous fp32 tensor
+    (on the GPU: one DMA each) is serialized from a pinned blob slot and
+    handed to the pickler uncopied, so a socket can send the weights straight
+    from the DMA target.  The caller holds ``LOCK`` until it is done with
+    the parts (the next call reuses the slots).  Other tensors pickle as
+    torch pickles them, from the host."""
+    out = _Parts()
+    pickle.Pickler(out, protocol=5).dump({"type": "global_model_update", "model": _placeholders(state),
+                                          "addr": addr, "port": port})
+    return out.parts
+
+
+def _placeholders(state):
+    """The state_dict with each contiguous fp32 tensor replaced by a _Tensor
+    over its freshly filled pinned blob slot (caller holds LOCK)."""
+    items = list(state.items())
+    fast = [(k, t) for k, t in items if t.dtype == torch.float32 and t.is_contiguous()]
+    model = collections.OrderedDict() if isinstance(state, collections.OrderedDict) else type(state)()
+    slots = {}
+    if fast:
+        dev = fast[0][1].device
+        sig = (str(dev), tuple(t.numel() for _, t in fast))
+        lay = _LAYOUTS.get(sig)
+        if lay is None:
+            lay = _Layout(sig[1], dev.type == "cuda")
+            _LAYOUTS.clear()  # one model per process: keep the latest layout only
+            _LAYOUTS[sig] = lay
+        for (k, t), (a, p, e) in zip(fast, lay.spans):
+            if t.numel():
+                lay.buf[p:e].copy_(t.detach().reshape(-1).view(torch.uint8), non_blocking=t.is_cuda)
+            slots[k] = (t, lay.mv[a:e])
+        for d in {t.device for _, t in fast if t.is_cuda}:
+            torch.cuda.current_stream(d).synchronize()
+    for k, t in items:
+        if k in slots:
+            src, mv = slots[k]
+            model[k] = _Tensor(_Blob(mv), tuple(src.shape), tuple(src.stride()))
+        else:
+            model[k] = t.detach().cpu()
+    return model
+
+
+def global_model_envelope(state, addr, port) -> bytes:
+    """The envelope as one bytes object: ``pickle.loads`` gives what the
+    reference's ``pickle.dumps({"type": "global_model_update", "model":
+    state, "addr": addr, "port": port})`` gives (one copy of the weights,
+    into the result)."""
+    with LOCK:
+        return b"".join(envelope_parts(state, addr, port))

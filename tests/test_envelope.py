@@ -1,0 +1,102 @@
+"""The broadcast envelope (p2pdl_amd.node.envelope):
+its storage blobs are byte-identical to torch's legacy storage pickling, and
+the envelope loads with pickle.loads (reference node/node.py:112) and with
+the product's restricted parser exactly like the reference's
+pickle.dumps({"type": "global_model_update", "model": state_dict, ...})
+(reference aggregator/aggregation.py:70)."""
+import collections
+import io
+import pickle
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from p2pdl_amd.node import envelope as E
+from p2pdl_amd.node.inbox import ZeroCopyParser
+
+
+def _torch_blob(t):
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        fn, (blob,) = t.storage().__reduce__()
+    assert fn is torch.storage._load_from_bytes
+    return blob
+
+
+@pytest.mark.parametrize("n", [0, 1, 6, 255, 256, 65_536, 100_003])
+def test_blob_header_is_torchs(n):
+    t = torch.arange(n, dtype=torch.float32)
+    blob = _torch_blob(t)
+    f = io.BytesIO(blob)
+    for _ in range(3):
+        pickle.Unpickler(f).load()
+    keys = []
+
+    class U(pickle.Unpickler):
+        def persistent_load(self, pid):
+            keys.append(pid[2])
+
+    U(f).load()
+    assert E.legacy_storage_header(n, keys[0]) + t.numpy().tobytes() == blob
+
+
+def _state():
+    return collections.OrderedDict([
+        ("fc.weight", torch.randn(33, 17)), ("fc.bias", torch.randn(33)),
+        ("bn.running_mean", torch.zeros(33)), ("bn.num_batches_tracked", torch.tensor(7)),
+        ("empty", torch.zeros(0)), ("strided", torch.randn(5, 3).t()), ("half", torch.randn(4).half()),
+    ])
+
+
+def test_envelope_loads_like_the_reference():
+    sd = _state()
+    ours = E.global_model_envelope(sd, "10.0.0.1", 5001)
+    ref = pickle.dumps({"type": "global_model_update", "model": sd, "addr": "10.0.0.1", "port": 5001})
+    a, b = pickle.loads(ours), pickle.loads(ref)
+    assert {k: v for k, v in a.items() if k != "model"} == {k: v for k, v in b.items() if k != "model"}
+    assert type(a["model"]) is collections.OrderedDict and list(a["model"]) == list(sd)
+    for k, v in sd.items():
+        got = a["model"][k]
+        assert got.dtype == v.dtype and got.shape == v.shape and got.stride() == v.stride(), k
+        assert torch.equal(got, v), k
+        assert got.untyped_storage().nbytes() == v.untyped_storage().nbytes(), k
+
+
+def test_envelope_parts_alias_the_slots_and_join_to_the_envelope():
+    sd = _state()
+    sd["big"] = torch.randn(200, 200)  # above the pickler's 64 KiB frame: handed over, not framed
+    with E.LOCK:
+        parts = E.envelope_parts(sd, "h", 1)
+        big = [p for p in parts if p.nbytes >= 200 * 200 * 4]
+        assert len(big) == 1 and not isinstance(big[0].obj, bytes)  # a view of the slot, not a copy
+        joined = b"".join(parts)
+    assert pickle.loads(joined)["model"].keys() == sd.keys()
+    assert joined == E.global_model_envelope(sd, "h", 1)
+
+
+def test_envelope_passes_the_restricted_parser():
+    """A peer running p2pdl_amd's receive path parses the global model with
+    the restricted machine (no unpickler on peer bytes): same payloads."""
+    sd = collections.OrderedDict((k, v) for k, v in _state().items() if k not in ("bn.num_batches_tracked",))
+    with E.LOCK:  # the model as the envelope encodes it (protocol 5, in-band blobs)
+        blob = pickle.dumps(E._placeholders(sd), protocol=5)
+    raw = ZeroCopyParser(blob).parse()
+    for k, v in sd.items():
+        arr = np.ascontiguousarray(raw[k].array()).reshape(-1)
+        assert np.array_equal(arr.view(np.uint8), v.contiguous().numpy().reshape(-1).view(np.uint8)), k
+
+
+@pytest.mark.gpu
+def test_envelope_from_gpu_model(cuda):
+    net = torch.nn.Sequential(torch.nn.Linear(33, 64), torch.nn.BatchNorm1d(64), torch.nn.Linear(64, 10)).to(cuda)
+    sd = net.state_dict()
+    for _ in range(2):  # the second call reuses the pinned layout
+        got = pickle.loads(E.global_model_envelope(sd, "a", 2))["model"]
+        assert list(got) == list(sd)
+        for k, v in sd.items():
+            assert torch.equal(got[k], v.cpu()) and got[k].device.type == "cpu", k
+        with torch.no_grad():
+            for p in net.parameters():
+                p.add_(1.0)  # new values, same layout
