@@ -186,7 +186,7 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
   }
   block_sync();  // 1: both max(lo)
   if constexpr (FLAGS) {  // block-wide: every pair of the block takes the same path (same barriers)
-    if (uniform((flags[0] | flags[1] | (NP > 1 ? flags[2] | flags[3] : 0)) != 0))
+    if (uniform((flags[0] | flags[1] | (NP > 1 ? flags[2] | flags[3] : 0) | (NP > 2 ? flags[4] | flags[5] : 0)) != 0))
       return pair_keys<P2P_RULE_MEDIAN, PAD>(P, c0, lane_off, im, h, lane, K, pd.lo, pd.m);
   }
   const T mo = from_raw<T>(part[(1 - h) * 64 + lane]);
@@ -254,7 +254,7 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   }
   block_sync();  // 1: both parities in the image
   if constexpr (FLAGS) {  // block-wide (same barriers for every pair)
-    if (uniform((flags[0] | flags[1] | (NP > 1 ? flags[2] | flags[3] : 0)) != 0))
+    if (uniform((flags[0] | flags[1] | (NP > 1 ? flags[2] | flags[3] : 0) | (NP > 2 ? flags[4] | flags[5] : 0)) != 0))
       return pair_keys<RULE, PAD>(P, c0, lane_off, im, h, lane, K, pd.lo, pd.m);
   }
   {
