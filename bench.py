@@ -965,9 +965,7 @@ def run_inbox_workload(args, K, n, seed, dev):
         return [inbox.digest(k) for k in range(len(msgs))]
 
     t_pin, t_pin_dig = timed(ours_pinned), timed(ours_pinned_digest)
-    # the broadcast's own path: the parts it sends (node.envelope.envelope_parts);
-    # the joined bytes object beside it
-    t_joined, t_ref, t_ours = timed(ours), timed(reference), timed(ours_parts)
+    t_ours, t_ref = timed(ours), timed(reference)
     t_dig, t_seq, t_ref_dig = timed(ours_digest), timed(land_then_hash), timed(reference_echo)
     n = sum(_numel(s) for _, s in shapes)
     nbytes = K * n * 4
