@@ -34,7 +34,7 @@ import threading
 import numpy as np
 import torch
 
-__all__ = ["LOCK", "envelope_parts", "global_model_envelope", "legacy_storage_header"]
+__all__ = ["LOCK", "dumps_state", "envelope_parts", "global_model_envelope", "legacy_storage_header"]
 
 # torch.serialization's legacy stream: magic number, protocol version, sys_info
 _MAGIC = 0x1950A86A20F9469CFC6C
@@ -129,6 +129,18 @@ class _Parts:
         return m.nbytes
 
 
+def _layout_for(purpose, fast):
+    dev = fast[0][1].device
+    sig = (purpose, str(dev), tuple(t.numel() for _, t in fast))
+    lay = _LAYOUTS.get(sig)
+    if lay is None:
+        lay = _Layout(sig[2], dev.type == "cuda")
+        for old in [k for k in _LAYOUTS if k[0] == purpose]:
+            del _LAYOUTS[old]  # one model per purpose: keep the latest layout only
+        _LAYOUTS[sig] = lay
+    return lay
+
+
 def envelope_parts(state, addr, port):
     """The global_model_update envelope as a list of buffers whose
     concatenation is its pickle (protocol 5): every contiguous fp32 tensor
@@ -143,7 +155,19 @@ def envelope_parts(state, addr, port):
     return out.parts
 
 
-def _placeholders(state):
+def dumps_state(state) -> bytes:
+    """``pickle.dumps(state)`` for a trainer's local update (reference
+    node/node.py:285) by the same route: each contiguous fp32 tensor DMA'd
+    into a pinned blob slot of its own layout (the trainer's, apart from
+    the global model's) and written once into the result.  ``pickle.loads``
+    and the inbox's parser read it as they read torch's pickle."""
+    with LOCK:
+        out = _Parts()
+        pickle.Pickler(out, protocol=5).dump(_placeholders(state, purpose="update"))
+        return b"".join(out.parts)
+
+
+def _placeholders(state, purpose="global"):
     """The state_dict with each contiguous fp32 tensor replaced by a _Tensor
     over its freshly filled pinned blob slot (caller holds LOCK)."""
     items = list(state.items())
@@ -151,13 +175,7 @@ def _placeholders(state):
     model = collections.OrderedDict() if isinstance(state, collections.OrderedDict) else type(state)()
     slots = {}
     if fast:
-        dev = fast[0][1].device
-        sig = (str(dev), tuple(t.numel() for _, t in fast))
-        lay = _LAYOUTS.get(sig)
-        if lay is None:
-            lay = _Layout(sig[1], dev.type == "cuda")
-            _LAYOUTS.clear()  # one model per process: keep the latest layout only
-            _LAYOUTS[sig] = lay
+        lay = _layout_for(purpose, fast)
         for (k, t), (a, p, e) in zip(fast, lay.spans):
             if t.numel():
                 lay.buf[p:e].copy_(t.detach().reshape(-1).view(torch.uint8), non_blocking=t.is_cuda)

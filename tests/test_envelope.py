@@ -88,6 +88,24 @@ def test_envelope_passes_the_restricted_parser():
         assert np.array_equal(arr.view(np.uint8), v.contiguous().numpy().reshape(-1).view(np.uint8)), k
 
 
+def test_dumps_state_is_a_state_dict_pickle():
+    """The trainer's update (reference node/node.py:285) by the same route:
+    pickle.loads and the restricted parser read the state back; the global
+    model's layout is left alone."""
+    sd = _state()
+    g = E.global_model_envelope(sd, "h", 1)
+    upd = collections.OrderedDict((k, v * 2) for k, v in sd.items() if v.dtype == torch.float32)
+    data = E.dumps_state(upd)
+    back = pickle.loads(data)
+    assert type(back) is collections.OrderedDict and list(back) == list(upd)
+    assert all(torch.equal(back[k], v) for k, v in upd.items())
+    raw = ZeroCopyParser(data).parse()
+    for k, v in upd.items():
+        arr = np.ascontiguousarray(raw[k].array()).reshape(-1)
+        assert np.array_equal(arr.view(np.uint8), v.contiguous().numpy().reshape(-1).view(np.uint8)), k
+    assert E.global_model_envelope(sd, "h", 1) == g  # its own layout, untouched
+
+
 @pytest.mark.gpu
 def test_envelope_from_gpu_model(cuda):
     net = torch.nn.Sequential(torch.nn.Linear(33, 64), torch.nn.BatchNorm1d(64), torch.nn.Linear(64, 10)).to(cuda)
