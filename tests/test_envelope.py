@@ -112,9 +112,11 @@ def test_envelope_from_gpu_model(cuda):
     sd = net.state_dict()
     for _ in range(2):  # the second call reuses the pinned layout
         got = pickle.loads(E.global_model_envelope(sd, "a", 2))["model"]
-        assert list(got) == list(sd)
+        upd = pickle.loads(E.dumps_state(sd))  # the trainer's route, its own layout
+        assert list(got) == list(sd) and list(upd) == list(sd)
         for k, v in sd.items():
             assert torch.equal(got[k], v.cpu()) and got[k].device.type == "cpu", k
+            assert torch.equal(upd[k], v.cpu()), k
         with torch.no_grad():
             for p in net.parameters():
                 p.add_(1.0)  # new values, same layout
