@@ -240,6 +240,72 @@ def _gpu_batch_wins(msgs) -> bool:
     return len(msgs) >= GPU_BATCH_MIN and max(len(m) for m in msgs) <= GPU_MAX_MESSAGE
 
 
+# Device-resident messages (cfg5: 256 x 100 MB in HBM): the same boundary.
+# Off the GPU kernel's side they cross PCIe in STAGE-byte pieces into pinned
+# buffers of the hashing thread that owns the message (two per thread, the
+# next piece in flight on the thread's own stream while it hashes the last):
+# the D2H (~50 GB/s) hides under the hashing (~2.4 GB/s per thread).
+STAGE = 8 << 20
+_TLS = threading.local()
+
+
+def _staging(dev):
+    st = getattr(_TLS, "stage", None)
+    if st is None or st[0] != dev:
+        import torch
+
+        st = (dev, torch.cuda.Stream(dev), [torch.empty(STAGE, dtype=torch.uint8, pin_memory=True) for _ in range(2)],
+              [torch.cuda.Event() for _ in range(2)])
+        _TLS.stage = st
+    return st
+
+
+def _hash_device_message(msgs, off: int, n: int, ready) -> bytes:
+    import torch
+
+    _, stream, bufs, evs = _staging(msgs.device)
+    stream.wait_event(ready)  # the messages as the caller's stream left them
+    h = hashlib.sha256()
+    pieces = [(o, min(STAGE, off + n - o)) for o in range(off, off + n, STAGE)]
+
+    def issue(i):
+        o, ln = pieces[i]
+        with torch.cuda.stream(stream):
+            bufs[i % 2][:ln].copy_(msgs[o:o + ln], non_blocking=True)
+            evs[i % 2].record(stream)
+
+    if pieces:
+        issue(0)
+    for i, (_, ln) in enumerate(pieces):
+        if i + 1 < len(pieces):
+            issue(i + 1)  # buffer (i + 1) % 2 held piece i - 1, hashed already
+        evs[i % 2].synchronize()
+        h.update(memoryview(bufs[i % 2].numpy())[:ln])
+    return h.digest()
+
+
+def digest_device_messages(msgs, offsets, lengths):
+    """SHA-256 of K messages in one device uint8 buffer, as a (K, 32) uint8
+    device tensor: the GPU batch kernel (``ops.sha256_batch_device``) for
+    GPU_BATCH_MIN or more messages of at most GPU_MAX_MESSAGE bytes, else the
+    host hashing threads with each message streamed over PCIe in STAGE-byte
+    pieces (for long messages one host thread hashes ~70x
+    faster than one GPU lane chain).  Synchronises on the host route."""
+    import torch
+
+    offsets, lengths = [int(o) for o in offsets], [int(x) for x in lengths]
+    if len(offsets) >= GPU_BATCH_MIN and max(lengths, default=0) <= GPU_MAX_MESSAGE:
+        from .. import ops
+
+        return ops.sha256_batch_device(msgs, offsets, lengths)
+    dev = msgs.device
+    ready = torch.cuda.Event()
+    ready.record(torch.cuda.current_stream(dev))
+    futs = [hash_pool().submit(_hash_device_message, msgs, o, n, ready) for o, n in zip(offsets, lengths)]
+    out = np.frombuffer(b"".join(f.result() for f in futs), dtype=np.uint8).reshape(len(offsets), 32)
+    return torch.from_numpy(out.copy()).to(dev)
+
+
 def digest_many(messages) -> list:
     """SHA-256 of every message, each distinct message hashed at most once:
     cached ones from the cache, the rest on the host threads or -- for
