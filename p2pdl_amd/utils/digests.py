@@ -173,6 +173,7 @@ class DigestCache:
 
 CACHE = DigestCache()
 _POOL = None
+_POOL_PREFIX = "p2p-sha256"
 _POOL_LOCK = threading.Lock()
 
 
@@ -183,7 +184,7 @@ def hash_pool():
         if _POOL is None:
             from concurrent.futures import ThreadPoolExecutor
 
-            _POOL = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1), thread_name_prefix="p2p-sha256")
+            _POOL = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1), thread_name_prefix=_POOL_PREFIX)
         return _POOL
 
 
@@ -301,8 +302,12 @@ def digest_device_messages(msgs, offsets, lengths):
     dev = msgs.device
     ready = torch.cuda.Event()
     ready.record(torch.cuda.current_stream(dev))
-    futs = [hash_pool().submit(_hash_device_message, msgs, o, n, ready) for o, n in zip(offsets, lengths)]
-    out = np.frombuffer(b"".join(f.result() for f in futs), dtype=np.uint8).reshape(len(offsets), 32)
+    if threading.current_thread().name.startswith(_POOL_PREFIX):  # a pool task waiting on the pool could deadlock
+        ds = [_hash_device_message(msgs, o, n, ready) for o, n in zip(offsets, lengths)]
+    else:
+        ds = [f.result() for f in [hash_pool().submit(_hash_device_message, msgs, o, n, ready)
+                                   for o, n in zip(offsets, lengths)]]
+    out = np.frombuffer(b"".join(ds), dtype=np.uint8).reshape(len(offsets), 32)
     return torch.from_numpy(out.copy()).to(dev)
 
 
