@@ -70,13 +70,15 @@ def _worker(rank, world, port, n, k, rule, chunk, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("rule,n,k,chunk", [("fedavg", 10_007, 5, 1000), ("fedavg", 4096, 3, 512),
-                                            ("median", 3001, 7, 256), ("trimmed", 777, 10, 100)])
-def test_gloo_world2_byte_identical_to_single(rule, n, k, chunk):
+@pytest.mark.parametrize("world,rule,n,k,chunk", [(2, "fedavg", 10_007, 5, 1000), (2, "fedavg", 4096, 3, 512),
+                                                  (2, "median", 3001, 7, 256), (2, "trimmed", 777, 10, 100),
+                                                  # the driver's 4-rank leg and an odd world, rehearsed on gloo
+                                                  (4, "fedavg", 10_007, 6, 300), (3, "median", 2049, 9, 128)])
+def test_gloo_world_byte_identical_to_single(world, rule, n, k, chunk):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, k, rule, chunk, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, k, rule, chunk, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=120) for _ in procs)
@@ -90,7 +92,7 @@ def test_gloo_world2_byte_identical_to_single(rule, n, k, chunk):
     else:
         rid = 1 if rule == "median" else 2
         want, _ = oracle.robust(peers, rid, oracle.trim_count(k) if rid == 2 else 0, w=w)
-    assert got[0] == got[1] == want.tobytes()
+    assert all(got[r] == want.tobytes() for r in range(world))
 
 
 # ---------------------------------------------------------------- GPU leg
