@@ -1175,8 +1175,8 @@ def run_broadcast_workload(args, seed, dev):
 
     if not args.no_check:
         a, b = pickle.loads(ours())["model"], pickle.loads(reference())["model"]
-        ok = list(a) == list(b) and all(torch.equal(a[k], b[k].cpu()) for k in b)
-        log(f"broadcast: host state_dict envelope == the reference's: {ok}")
+        ok = list(a) == list(b) and all(a[k].device == b[k].device and torch.equal(a[k], b[k]) for k in b)
+        log(f"broadcast: envelope == the reference's (payloads, devices): {ok}")
         if not ok:
             raise SystemExit("bench: broadcast payload differs from the reference's")
 

@@ -22,7 +22,10 @@ broadcast sends the weights straight from the DMA target
 receiver's ``pickle.loads`` (reference node/node.py:112) and
 ``p2pdl_amd.node.inbox.ZeroCopyParser`` read it like torch's own pickle
 (``tests/test_envelope.py`` checks the blobs against ``torch.save`` byte for
-byte and the envelope against ``pickle.loads``).
+byte and the envelope against ``pickle.loads``).  Each blob names its
+storage's own location, as torch's does ('cuda:0' for the reference's GPU
+model), so ``pickle.loads`` puts every tensor on the device the reference's
+envelope puts it on.
 """
 from __future__ import annotations
 
@@ -47,10 +50,11 @@ class _StorageRef:
     """Stands for the storage in the header's persistent-id pickle."""
 
 
-def legacy_storage_header(numel: int, key: str) -> bytes:
+def legacy_storage_header(numel: int, key: str, location: str = "cpu") -> bytes:
     """The bytes torch's legacy ``torch.save`` of a float32 storage of
-    ``numel`` elements writes before the raw data: the four header pickles
-    (protocol 2, as torch writes them), the key list and the 8-byte count."""
+    ``numel`` elements on ``location`` ('cpu', 'cuda:0', ...) writes before
+    the raw data: the four header pickles (protocol 2, as torch writes them),
+    the key list and the 8-byte count."""
     f = io.BytesIO()
     pickle.dump(_MAGIC, f, protocol=2)
     pickle.dump(_PROTOCOL_VERSION, f, protocol=2)
@@ -60,7 +64,7 @@ def legacy_storage_header(numel: int, key: str) -> bytes:
     class _P(pickle.Pickler):
         def persistent_id(self, obj):
             if obj is ref:
-                return ("storage", torch.FloatStorage, key, "cpu", numel, None)
+                return ("storage", torch.FloatStorage, key, location, numel, None)
             return None
 
     _P(f, protocol=2).dump(ref)
@@ -94,10 +98,11 @@ class _Tensor:
 
 
 class _Layout:
-    """One pinned buffer of legacy blobs for a fixed list of fp32 sizes."""
+    """One pinned buffer of legacy blobs for a fixed list of fp32 sizes and
+    storage locations."""
 
-    def __init__(self, numels, pin: bool):
-        heads = [legacy_storage_header(n, str(i)) for i, n in enumerate(numels)]
+    def __init__(self, numels, locations, pin: bool):
+        heads = [legacy_storage_header(n, str(i), loc) for i, (n, loc) in enumerate(zip(numels, locations))]
         self.spans = []  # (blob start, payload start, blob end) per tensor
         off = 0
         for h, n in zip(heads, numels):
@@ -130,11 +135,11 @@ class _Parts:
 
 
 def _layout_for(purpose, fast):
-    dev = fast[0][1].device
-    sig = (purpose, str(dev), tuple(t.numel() for _, t in fast))
+    locs = tuple(torch.serialization.location_tag(t.untyped_storage()) for _, t in fast)
+    sig = (purpose, locs, tuple(t.numel() for _, t in fast))
     lay = _LAYOUTS.get(sig)
     if lay is None:
-        lay = _Layout(sig[2], dev.type == "cuda")
+        lay = _Layout(sig[2], locs, any(t.is_cuda for _, t in fast))
         for old in [k for k in _LAYOUTS if k[0] == purpose]:
             del _LAYOUTS[old]  # one model per purpose: keep the latest layout only
         _LAYOUTS[sig] = lay
@@ -187,7 +192,7 @@ def _placeholders(state, purpose="global"):
             src, mv = slots[k]
             model[k] = _Tensor(_Blob(mv), tuple(src.shape), tuple(src.stride()))
         else:
-            model[k] = t.detach().cpu()
+            model[k] = t.detach()  # pickled by torch, as the reference pickles it
     return model
 
 

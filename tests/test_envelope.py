@@ -42,6 +42,32 @@ def test_blob_header_is_torchs(n):
     assert E.legacy_storage_header(n, keys[0]) + t.numpy().tobytes() == blob
 
 
+def _blob_key_location(blob):
+    f = io.BytesIO(blob)
+    for _ in range(3):
+        pickle.Unpickler(f).load()
+    pids = []
+
+    class U(pickle.Unpickler):
+        def persistent_load(self, pid):
+            pids.append(pid)
+
+    U(f).load()
+    return pids[0][2], pids[0][3]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 255, 100_003])
+def test_blob_header_is_torchs_on_the_gpu(cuda, n):
+    """A CUDA storage's blob names its location ('cuda:0'), as torch's
+    pickle of the reference's GPU state_dict does."""
+    t = torch.arange(n, dtype=torch.float32, device=cuda)
+    blob = _torch_blob(t)
+    key, loc = _blob_key_location(blob)
+    assert loc == torch.serialization.location_tag(t.untyped_storage()) and loc.startswith("cuda:")
+    assert E.legacy_storage_header(n, key, loc) + t.cpu().numpy().tobytes() == blob
+
+
 def _state():
     return collections.OrderedDict([
         ("fc.weight", torch.randn(33, 17)), ("fc.bias", torch.randn(33)),
@@ -114,9 +140,10 @@ def test_envelope_from_gpu_model(cuda):
         got = pickle.loads(E.global_model_envelope(sd, "a", 2))["model"]
         upd = pickle.loads(E.dumps_state(sd))  # the trainer's route, its own layout
         assert list(got) == list(sd) and list(upd) == list(sd)
+        ref = pickle.loads(pickle.dumps({"model": sd}))["model"]  # the reference's envelope
         for k, v in sd.items():
-            assert torch.equal(got[k], v.cpu()) and got[k].device.type == "cpu", k
-            assert torch.equal(upd[k], v.cpu()), k
+            assert got[k].device == ref[k].device == v.device and upd[k].device == v.device, k
+            assert torch.equal(got[k], v) and torch.equal(upd[k], v), k
         with torch.no_grad():
             for p in net.parameters():
                 p.add_(1.0)  # new values, same layout
