@@ -450,11 +450,39 @@ def delta_snapshot_segments_(curs: Sequence[torch.Tensor], prevs: Sequence[torch
 
 
 # ------------------------------------------------------------------ K3
+def _check_tensor(t: torch.Tensor, name: str, dtypes, shape, dev, min_numel: int = 0) -> None:
+    dtypes = dtypes if isinstance(dtypes, tuple) else (dtypes,)
+    if t.dtype not in dtypes or not t.is_contiguous() or t.device != dev:
+        raise ValueError(f"{name} must be a contiguous {'/'.join(str(d) for d in dtypes)} tensor on {dev}, "
+                         f"got {t.dtype} on {t.device}")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+    if t.numel() < min_numel:
+        raise ValueError(f"{name} has {t.numel()} elements, needs at least {min_numel}")
+
+
+def check_message_spans(msgs: torch.Tensor, offsets: Sequence[int], lengths: Sequence[int]) -> None:
+    """Messages [offset, offset + length) of a contiguous 1-D uint8 buffer:
+    raises ValueError for any span outside it."""
+    if msgs.dtype != torch.uint8 or msgs.dim() != 1 or not msgs.is_contiguous():
+        raise ValueError(f"messages must be a contiguous 1-D uint8 tensor, got {msgs.dtype} {tuple(msgs.shape)}")
+    if len(offsets) != len(lengths):
+        raise ValueError(f"{len(offsets)} offsets for {len(lengths)} lengths")
+    size = msgs.numel()
+    for j, (o, n) in enumerate(zip(offsets, lengths)):
+        o, n = int(o), int(n)
+        if o < 0 or n < 0 or o + n > size:
+            raise ValueError(f"message {j}: bytes [{o}, {o + n}) outside the {size}-byte buffer")
+
+
 def sha256_batch_device(msgs: torch.Tensor, offsets: Sequence[int], lengths: Sequence[int]) -> torch.Tensor:
     """Digest K messages that live in one device uint8 buffer.
 
-    Returns a (K, 32) uint8 device tensor; does not synchronise."""
+    Returns a (K, 32) uint8 device tensor; does not synchronise.  Every
+    message must lie inside ``msgs`` (ValueError otherwise: the kernel reads
+    raw addresses)."""
     N.require_device(msgs)
+    check_message_spans(msgs, offsets, lengths)
     dev = msgs.device
     K = len(offsets)
     digests = torch.empty((max(K, 1), 32), dtype=torch.uint8, device=dev)
@@ -498,8 +526,17 @@ def sha256_batch(messages: Sequence[bytes], device=None) -> list[bytes]:
 
 def digest_accept(digests: torch.Tensor, expected: torch.Tensor, payload_table: torch.Tensor,
                   accepted: torch.Tensor, count: torch.Tensor) -> None:
-    """accepted[0:count] = payloads whose digest matches, in list order (device)."""
+    """accepted[0:count] = payloads whose digest matches, in list order (device).
+    Shapes are checked here (the kernel reads raw addresses): digests and
+    expected (k, 32) uint8, payload_table / accepted k 8-byte pointers,
+    count one int32, all on one device."""
     k = payload_table.numel()
+    dev = digests.device
+    _check_tensor(digests, "digests", torch.uint8, (k, 32), dev)
+    _check_tensor(expected, "expected", torch.uint8, (k, 32), dev)
+    _check_tensor(payload_table, "payload_table", (torch.int64, torch.uint64), (k,), dev)
+    _check_tensor(accepted, "accepted", (torch.int64, torch.uint64), None, dev, min_numel=k)
+    _check_tensor(count, "count", torch.int32, None, dev, min_numel=1)
     with torch.cuda.device(digests.device):
         N.check(N.lib().p2p_digest_accept(digests.data_ptr(), expected.data_ptr(),
                                           payload_table.data_ptr(), k, accepted.data_ptr(),
@@ -508,7 +545,19 @@ def digest_accept(digests: torch.Tensor, expected: torch.Tensor, payload_table: 
 
 def fedavg_apply_devk_(w: torch.Tensor, table: torch.Tensor, k_dev: torch.Tensor, k_max: int,
                        lr: float = 0.1, out: torch.Tensor | None = None) -> None:
-    """FedAvg over table[0:*k_dev] with the peer count read on the device."""
+    """FedAvg over table[0:*k_dev] with the peer count read on the device
+    (1 <= *k_dev <= k_max, the caller's contract: the count is not read on
+    the host).  table holds at least k_max 8-byte pointers."""
+    dev = w.device
+    _check_f32(w, "w", dev)
+    if out is not None:
+        _check_f32(out, "out", dev)
+        if out.numel() != w.numel():
+            raise ValueError(f"out has {out.numel()} elements, w {w.numel()}")
+    if not 1 <= k_max:
+        raise ValueError(f"k_max must be >= 1, got {k_max}")
+    _check_tensor(table, "table", (torch.int64, torch.uint64), None, dev, min_numel=k_max)
+    _check_tensor(k_dev, "k_dev", torch.int32, None, dev, min_numel=1)
     with torch.cuda.device(w.device):
         N.check(N.lib().p2p_fedavg_apply_devk_f32(table.data_ptr(), k_dev.data_ptr(), k_max, w.numel(),
                                                   w.data_ptr(), lr,

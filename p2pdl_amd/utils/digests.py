@@ -294,10 +294,11 @@ def digest_device_messages(msgs, offsets, lengths):
     faster than one GPU lane chain).  Synchronises on the host route."""
     import torch
 
-    offsets, lengths = [int(o) for o in offsets], [int(x) for x in lengths]
-    if len(offsets) >= GPU_BATCH_MIN and max(lengths, default=0) <= GPU_MAX_MESSAGE:
-        from .. import ops
+    from .. import ops
 
+    offsets, lengths = [int(o) for o in offsets], [int(x) for x in lengths]
+    ops.check_message_spans(msgs, offsets, lengths)
+    if len(offsets) >= GPU_BATCH_MIN and max(lengths, default=0) <= GPU_MAX_MESSAGE:
         return ops.sha256_batch_device(msgs, offsets, lengths)
     dev = msgs.device
     ready = torch.cuda.Event()

@@ -46,3 +46,52 @@ def test_device_message_digests_see_the_callers_stream(cuda):
         dev.fill_(7)
         got = dg.digest_device_messages(dev, [0], [n]).cpu().numpy()
     assert bytes(got[0]) == hashlib.sha256(bytes([7]) * n).digest()
+
+
+@pytest.mark.parametrize("offsets,lengths,why", [
+    ([0, 90], [10, 11], "outside"),     # ends one byte past the buffer
+    ([-1], [4], "outside"),             # negative offset
+    ([0], [-1], "outside"),             # negative length
+    ([0, 1], [1], "offsets for"),       # count mismatch
+])
+def test_message_spans_are_checked_before_any_device_read(offsets, lengths, why):
+    """The kernel reads raw addresses: a span outside the buffer is a
+    ValueError on the host, never a launch (no GPU needed to check)."""
+    from p2pdl_amd import ops
+
+    buf = torch.zeros(100, dtype=torch.uint8)
+    with pytest.raises(ValueError, match=why):
+        ops.check_message_spans(buf, offsets, lengths)
+    ops.check_message_spans(buf, [0, 90, 100], [90, 10, 0])  # the edges themselves are inside
+
+
+@pytest.mark.parametrize("bad", [torch.zeros(8, dtype=torch.float32), torch.zeros((2, 8), dtype=torch.uint8),
+                                 torch.zeros(16, dtype=torch.uint8)[::2]])
+def test_message_buffer_must_be_flat_bytes(bad):
+    from p2pdl_amd import ops
+
+    with pytest.raises(ValueError, match="contiguous 1-D uint8"):
+        ops.check_message_spans(bad, [0], [1])
+
+
+def test_fused_path_wrappers_check_shapes_before_the_launch():
+    """digest_accept / fedavg_apply_devk_ pass raw addresses to kernels that
+    index k rows: a mis-sized operand is a ValueError on the host (checked
+    here with host tensors; the checks run before any native call)."""
+    from p2pdl_amd import ops
+
+    k = 4
+    dig, exp = torch.zeros((k, 32), dtype=torch.uint8), torch.zeros((k, 32), dtype=torch.uint8)
+    tbl, acc, cnt = torch.zeros(k, dtype=torch.int64), torch.zeros(k, dtype=torch.int64), torch.zeros(1, dtype=torch.int32)
+    for args, what in [((dig[:3], exp, tbl, acc, cnt), "digests"), ((dig, exp[:, :16], tbl, acc, cnt), "expected"),
+                       ((dig, exp, tbl, acc[:3], cnt), "accepted"), ((dig, exp, tbl, acc, cnt[:0]), "count"),
+                       ((dig, exp, tbl.int(), acc, cnt), "payload_table")]:
+        with pytest.raises(ValueError, match=what):
+            ops.digest_accept(*args)
+    w = torch.zeros(10)
+    with pytest.raises(ValueError, match="table"):
+        ops.fedavg_apply_devk_(w, tbl[:2], cnt, 3)
+    with pytest.raises(ValueError, match="k_dev"):
+        ops.fedavg_apply_devk_(w, tbl, cnt.long(), 3)
+    with pytest.raises(ValueError, match="out has"):
+        ops.fedavg_apply_devk_(w, tbl, cnt, 3, out=torch.zeros(9))
