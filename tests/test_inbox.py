@@ -399,7 +399,7 @@ def test_broadcast_from_gpu_model_one_transfer(cuda):
     ref = net.state_dict()
     assert list(msg["model"]) == list(ref)
     for k, v in ref.items():
-        assert torch.equal(msg["model"][k], v.cpu()), k
+        assert msg["model"][k].device == v.device and torch.equal(msg["model"][k], v), k  # as the reference's pickle
         assert msg["model"][k].untyped_storage().nbytes() == v.numel() * v.element_size(), k
 
 
