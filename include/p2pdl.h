@@ -34,7 +34,7 @@ extern "C" {
 /* 2: p2p_set_robust_layout (a process-global A/B switch of version 1) is
  *    gone; every other entry point is unchanged.
  * 3: adds p2p_land_segments_f32 (K5, landing a received update). */
-#define P2P_ABI_VERSION 3
+#define P2P_ABI_VERSION 4
 
 typedef void *p2p_stream_t; /* hipStream_t */
 
@@ -45,7 +45,12 @@ enum {
   P2P_ERR_ALIGN = -3        /* a float pointer that is not 4-byte aligned */
 };
 
-enum { P2P_RULE_FEDAVG = 0, P2P_RULE_MEDIAN = 1, P2P_RULE_TRIMMED = 2 };
+/* P2P_RULE_FEDAVG: the reference's ops as torch runs them on CPU tensors
+ * (acc / K, IEEE division; the committed golden vectors).
+ * P2P_RULE_FEDAVG_TORCH_GPU: the same ops as torch runs them on GPU tensors,
+ * the reference's own deployment (node/node.py:28-29 puts the model on
+ * cuda): ATen divides by the CPU scalar K as acc * fl(1/K) (ABI 4). */
+enum { P2P_RULE_FEDAVG = 0, P2P_RULE_MEDIAN = 1, P2P_RULE_TRIMMED = 2, P2P_RULE_FEDAVG_TORCH_GPU = 3 };
 
 /* One tensor of a state_dict (reference: one key of self.model.state_dict(),
  * aggregator/aggregation.py:15,27,37).  Device-resident table entry. */

@@ -54,6 +54,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_synth_f32.restype = None
         L.oracle_fedavg_f32.argtypes = [P, ctypes.c_int32, ctypes.c_int64, P, ctypes.c_float, P]
         L.oracle_fedavg_f32.restype = None
+        L.oracle_fedavg_mode_f32.argtypes = [P, ctypes.c_int32, ctypes.c_int64, P, ctypes.c_float, P,
+                                             ctypes.c_int32]
+        L.oracle_fedavg_mode_f32.restype = None
         L.oracle_robust_f32.argtypes = [P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                                         ctypes.c_int32, P, ctypes.c_float, P]
         L.oracle_robust_f32.restype = ctypes.c_int
@@ -114,25 +117,28 @@ def synth_at(idx, seed: int, peer: int, scale: float) -> np.ndarray:
 
 
 # ---------------------------------------------------------------- FedAvg
-def fedavg(peers, w=None, lr: float = 0.1, want_out: bool = False):
+def fedavg(peers, w=None, lr: float = 0.1, want_out: bool = False, torch_gpu: bool = False):
     """C restatement of reference aggregator/aggregation.py:15-38.
+    torch_gpu: the ops as torch runs them on GPU tensors (acc * fl(1/K) at
+    :32; the product's 'fedavg_torch_gpu' rule).
 
     Returns (w_new, out) where w_new is a new array (input untouched)."""
     arrs, tbl = _peer_table(peers)
     n = arrs[0].size if arrs else 0
     w_new = None if w is None else np.array(w, dtype=np.float32, copy=True)
     out = np.empty(n, dtype=np.float32) if (want_out or w is None) else None
-    lib().oracle_fedavg_f32(tbl, len(arrs), n, None if w_new is None else _ptr(w_new),
-                            lr, None if out is None else _ptr(out))
+    lib().oracle_fedavg_mode_f32(tbl, len(arrs), n, None if w_new is None else _ptr(w_new),
+                                 lr, None if out is None else _ptr(out), int(torch_gpu))
     return w_new, out
 
 
-def fedavg_np(peers, w=None, lr: float = 0.1):
+def fedavg_np(peers, w=None, lr: float = 0.1, torch_gpu: bool = False):
     """numpy restatement (vectorised over coordinates, same op order)."""
     acc = np.zeros_like(np.asarray(peers[0], dtype=np.float32))
     for p in peers:
         acc = acc + np.asarray(p, dtype=np.float32)
-    acc = acc / np.float32(len(peers))
+    k = np.float32(len(peers))
+    acc = acc * (np.float32(1.0) / k) if torch_gpu else acc / k
     if w is None:
         return None, acc
     return (np.asarray(w, dtype=np.float32) + np.float32(lr) * acc).astype(np.float32), acc

@@ -20,8 +20,10 @@ Semantics preserved:
     (:25-38) -- bit-exact with the reference on CPU;
   * then received_models.clear() (:43) and broadcast (:46).
 Build extensions (keyword-only, defaults reproduce the reference): ``rule``
-('fedavg' | 'median' | 'trimmed', README.md:10 "Byzantine fault" TODO),
-``lr`` (:36) and ``trim_frac``.
+('fedavg' | 'median' | 'trimmed', README.md:10 "Byzantine fault" TODO, or
+'fedavg_torch_gpu': FedAvg bit-exact with the reference as torch runs it on
+GPU tensors -- its deployment, node/node.py:28-29 -- where :32 is
+acc * fl(1/K)), ``lr`` (:36) and ``trim_frac``.
 """
 import logging
 import pickle

@@ -5,14 +5,16 @@ extern "C" int64_t p2p_fedavg_tile_elems(void);
 extern "C" int64_t p2p_robust_tile_elems(int32_t rule, int32_t k);
 extern "C" int32_t p2p_fedavg_segments_f32(const p2p_segment_t* segs, int32_t nseg,
                                            int64_t total_tiles, int32_t k, float lr,
-                                           p2p_stream_t stream);
+                                           p2p_stream_t stream, int32_t recip);
 extern "C" int32_t p2p_robust_dispatch(const float* const* peers, const p2p_segment_t* segs,
                                        int32_t nseg, int64_t tiles, int32_t k, int32_t rule,
                                        int32_t trim_b, int64_t n, float* w, float* out, float lr,
                                        p2p_stream_t stream);
 
 int32_t p2p_fedavg_flat_launch(const float* const* peers, int32_t k, int64_t n, float* w, float* out,
-                               float lr, p2p_stream_t stream);
+                               float lr, p2p_stream_t stream, int32_t recip);
+
+static bool is_fedavg(int32_t rule) { return rule == P2P_RULE_FEDAVG || rule == P2P_RULE_FEDAVG_TORCH_GPU; }
 
 extern "C" int32_t p2p_abi_version(void) { return P2P_ABI_VERSION; }
 
@@ -29,7 +31,7 @@ extern "C" const char* p2p_strerror(int32_t code) {
 }
 
 extern "C" int64_t p2p_tile_elems(int32_t rule, int32_t k) {
-  return rule == P2P_RULE_FEDAVG ? p2p_fedavg_tile_elems() : p2p_robust_tile_elems(rule, k);
+  return is_fedavg(rule) ? p2p_fedavg_tile_elems() : p2p_robust_tile_elems(rule, k);
 }
 
 static bool misaligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) != 0; }
@@ -56,9 +58,9 @@ extern "C" int32_t p2p_aggregate_f32(const float* const* peers, int32_t k, int64
                                      p2p_stream_t stream) {
   if (!peers || (!w && !out) || k < 1 || n < 0) return P2P_ERR_INVALID;
   if (misaligned4(w) || misaligned4(out)) return P2P_ERR_ALIGN;
-  if (rule == P2P_RULE_FEDAVG) {
+  if (is_fedavg(rule)) {
     if (n == 0) return P2P_OK;
-    return p2p_fedavg_flat_launch(peers, k, n, w, out, lr, stream);
+    return p2p_fedavg_flat_launch(peers, k, n, w, out, lr, stream, rule == P2P_RULE_FEDAVG_TORCH_GPU);
   }
   if (rule != P2P_RULE_MEDIAN && rule != P2P_RULE_TRIMMED) return P2P_ERR_INVALID;
   if (rule == P2P_RULE_TRIMMED && (trim_b < 0 || k - 2 * trim_b <= 0)) return P2P_ERR_INVALID;
@@ -71,7 +73,8 @@ extern "C" int32_t p2p_aggregate_segments_f32(const p2p_segment_t* segs, int32_t
                                               int32_t trim_b, float lr, p2p_stream_t stream) {
   if (!segs || nseg < 1 || k < 1 || total_tiles < 0) return P2P_ERR_INVALID;
   if (total_tiles > 0x7FFFFFFFll) return P2P_ERR_UNSUPPORTED;
-  if (rule == P2P_RULE_FEDAVG) return p2p_fedavg_segments_f32(segs, nseg, total_tiles, k, lr, stream);
+  if (is_fedavg(rule))
+    return p2p_fedavg_segments_f32(segs, nseg, total_tiles, k, lr, stream, rule == P2P_RULE_FEDAVG_TORCH_GPU);
   if (rule != P2P_RULE_MEDIAN && rule != P2P_RULE_TRIMMED) return P2P_ERR_INVALID;
   if (total_tiles == 0) return P2P_OK;
   return p2p_robust_dispatch(nullptr, segs, nseg, total_tiles, k, rule, trim_b, 0, nullptr, nullptr, lr,

@@ -5,6 +5,11 @@
 //   for upd in received_models: acc += upd[key]  (:25-28) -> fixed peer order
 //   acc /= num_updates                           (:31-32) -> IEEE true division
 //   state_dict()[key] += 0.1 * acc               (:36-38) -> mul rounded, add rounded
+// P2P_RULE_FEDAVG_TORCH_GPU (RECIP below) reproduces the same ops as torch
+// runs them on a GPU tensor -- the reference's own deployment, the model on
+// cuda (node/node.py:28-29): ATen divides by a CPU scalar as a multiply by
+// fl(1/K) (measured on MI355X, tools/torch_div_probe.py: 20-54% of elements
+// differ from the true quotient at K = 3, 7, 10, 100).
 //
 // The reference issues K*L separate add_ kernels, each reading acc + update and
 // writing acc (3x the algorithmic traffic).  Here one pass reads every peer
@@ -42,9 +47,17 @@ __device__ __forceinline__ f4 ld_nt(const float* p) { return ldg_nt(reinterpret_
 __device__ __forceinline__ f4 ld(const float* p) { return ldg(reinterpret_cast<const f4*>(p)); }
 __device__ __forceinline__ void st(float* p, f4 v) { stg(reinterpret_cast<f4*>(p), v); }
 
-__device__ __forceinline__ f4 div4(f4 a, float k) {
+// acc / K (:31-32): IEEE division, or (RECIP) torch's GPU form acc * fl(1/K)
+// with inv = 1.0f / K correctly rounded (-fhip-fp32-correctly-rounded-divide-sqrt).
+template <bool RECIP>
+__device__ __forceinline__ float div1(float a, float k, float inv) {
+  return RECIP ? __fmul_rn(a, inv) : a / k;
+}
+template <bool RECIP>
+__device__ __forceinline__ f4 div4(f4 a, float k, float inv) {
   f4 r;
-  r.x = a.x / k; r.y = a.y / k; r.z = a.z / k; r.w = a.w / k;
+  r.x = div1<RECIP>(a.x, k, inv); r.y = div1<RECIP>(a.y, k, inv);
+  r.z = div1<RECIP>(a.z, k, inv); r.w = div1<RECIP>(a.w, k, inv);
   return r;
 }
 __device__ __forceinline__ f4 apply4(f4 w, float lr, f4 m) {
@@ -59,11 +72,12 @@ __device__ __forceinline__ f4 apply4(f4 w, float lr, f4 m) {
 // complete float4 groups still use vector loads under a per-lane predicate;
 // the <= 3 trailing elements of the array go element by element.  Same op
 // order on every path.
-template <int NV, bool FULL>
+template <int NV, bool FULL, bool RECIP>
 __device__ __forceinline__ void fedavg_tile_vec(const float* const* __restrict__ peers, int K,
                                                 int64_t n, int64_t base, float* w, float* out,
                                                 float lr) {
   const float fk = static_cast<float>(K);
+  const float inv = RECIP ? 1.0f / fk : 0.f;
   bool ok[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) ok[v] = FULL || (base + kBlock * 4 * v + 4 <= n);
@@ -95,31 +109,33 @@ __device__ __forceinline__ void fedavg_tile_vec(const float* const* __restrict__
   for (int v = 0; v < NV; ++v) {
     if (!ok[v]) continue;
     const int64_t o = base + kBlock * 4 * v;
-    const f4 m = div4(acc[v], fk);  // (:31-32)
+    const f4 m = div4<RECIP>(acc[v], fk, inv);  // (:31-32)
     if (out) st(out + o, m);
     if (w) st(w + o, apply4(ld(w + o), lr, m));  // (:36-38)
   }
 }
 
 // Element-wise path (misaligned views, and the < 4 trailing elements).
+template <bool RECIP>
 __device__ __forceinline__ void fedavg_elem(const float* const* __restrict__ peers, int K, int64_t i,
                                             float* w, float* out, float lr) {
   float acc = 0.f;
 #pragma unroll 8
   for (int k = 0; k < K; ++k) acc += ldg(table_at(peers, k) + i);
-  const float m = acc / static_cast<float>(K);
+  const float fk = static_cast<float>(K);
+  const float m = div1<RECIP>(acc, fk, RECIP ? 1.0f / fk : 0.f);
   if (out) stg(out + i, m);
   if (w) stg(w + i, apply_lr(ldg(w + i), lr, m));
 }
 
-template <int NV>
+template <int NV, bool RECIP>
 __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ peers, int K,
                                             int64_t n, int64_t tile0, float* w, float* out,
                                             float lr, bool aligned) {
   const int64_t base = tile0 + 4 * static_cast<int64_t>(threadIdx.x);
   if (aligned) {
     if (tile0 + tile_of<NV>() <= n) {
-      fedavg_tile_vec<NV, true>(peers, K, n, base, w, out, lr);
+      fedavg_tile_vec<NV, true, RECIP>(peers, K, n, base, w, out, lr);
       return;
     }
     // ragged last tile: 1024-float sub-tiles (same per-element op order)
@@ -127,9 +143,9 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
     for (int v = 0; v < NV; ++v) {
       const int64_t g = base + kBlock * 4 * v;
       if (tile0 + kBlock * 4 * v >= n) break;
-      fedavg_tile_vec<1, false>(peers, K, n, g, w, out, lr);
+      fedavg_tile_vec<1, false, RECIP>(peers, K, n, g, w, out, lr);
       if (g < n && g + 4 > n)  // trailing elements of a float4 group that straddles n
-        for (int64_t i = g; i < n; ++i) fedavg_elem(peers, K, i, w, out, lr);
+        for (int64_t i = g; i < n; ++i) fedavg_elem<RECIP>(peers, K, i, w, out, lr);
     }
     return;
   }
@@ -138,13 +154,13 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
 #pragma unroll 1
     for (int e = 0; e < 4; ++e) {
       const int64_t i = base + kBlock * 4 * v + e;
-      if (i < n) fedavg_elem(peers, K, i, w, out, lr);
+      if (i < n) fedavg_elem<RECIP>(peers, K, i, w, out, lr);
     }
 }
 
 // Flat buffer, one tile per block.  K either from the kernarg or, when
 // k_dev != nullptr, from device memory (fused accept -> FedAvg path).
-template <int NV>
+template <int NV, bool RECIP>
 __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const* __restrict__ peers,
                                                              int K, const int32_t* k_dev,
                                                              int64_t n, float* w, float* out,
@@ -152,16 +168,17 @@ __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const*
   if (k_dev) K = *k_dev;
   if (K <= 0) return;
   const bool aligned = all_aligned16(peers, K, w, out);
-  fedavg_tile<NV>(peers, K, n, static_cast<int64_t>(blockIdx.x) * tile_of<NV>(), w, out, lr, aligned);
+  fedavg_tile<NV, RECIP>(peers, K, n, static_cast<int64_t>(blockIdx.x) * tile_of<NV>(), w, out, lr, aligned);
 }
 
 // Whole state_dict: one tile per block, segment found by binary search.
+template <bool RECIP>
 __global__ __launch_bounds__(kBlock) void fedavg_segments_kernel(const Seg* __restrict__ segs,
                                                                  int nseg, int K, float lr) {
   const int64_t t = blockIdx.x;
   const Seg s = load_segment(segs, nseg, t);
   const bool aligned = all_aligned16(s.peers, K, s.w, s.out);
-  fedavg_tile<kNV>(s.peers, K, s.n, (t - s.tile_begin) * kTile, s.w, s.out, lr, aligned);
+  fedavg_tile<kNV, RECIP>(s.peers, K, s.n, (t - s.tile_begin) * kTile, s.w, s.out, lr, aligned);
 }
 
 __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* agg, float lr,
@@ -180,9 +197,12 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* ag
 static int grid_for_tiles(int64_t ntiles) { return static_cast<int>(ntiles > 0 ? ntiles : 1); }
 
 static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,
-                        float lr, hipStream_t stream) {
-  hipLaunchKernelGGL(fedavg_flat_kernel<kNV>, dim3(grid_for_tiles(ceil_div(n, kTile))), dim3(kBlock), 0, stream,
-                     peers, K, k_dev, n, w, out, lr);
+                        float lr, hipStream_t stream, bool recip = false) {
+  const dim3 grid(grid_for_tiles(ceil_div(n, kTile)));
+  if (recip)
+    hipLaunchKernelGGL((fedavg_flat_kernel<kNV, true>), grid, dim3(kBlock), 0, stream, peers, K, k_dev, n, w, out, lr);
+  else
+    hipLaunchKernelGGL((fedavg_flat_kernel<kNV, false>), grid, dim3(kBlock), 0, stream, peers, K, k_dev, n, w, out, lr);
 }
 
 static int grid_stride_blocks(int64_t nblocks) {
@@ -202,8 +222,8 @@ static int32_t launch_status() {
 extern "C" P2P_INTERNAL int64_t p2p_fedavg_tile_elems(void) { return kTile; }
 
 P2P_INTERNAL int32_t p2p_fedavg_flat_launch(const float* const* peers, int32_t k, int64_t n, float* w,
-                                            float* out, float lr, p2p_stream_t stream) {
-  launch_flat(peers, k, nullptr, n, w, out, lr, static_cast<hipStream_t>(stream));
+                                            float* out, float lr, p2p_stream_t stream, int32_t recip) {
+  launch_flat(peers, k, nullptr, n, w, out, lr, static_cast<hipStream_t>(stream), recip != 0);
   return launch_status();
 }
 
@@ -237,11 +257,16 @@ extern "C" int32_t p2p_fedavg_apply_devk_f32(const float* const* peers, const in
 
 extern "C" P2P_INTERNAL int32_t p2p_fedavg_segments_f32(const p2p_segment_t* segs, int32_t nseg,
                                            int64_t total_tiles, int32_t k, float lr,
-                                           p2p_stream_t stream) {
+                                           p2p_stream_t stream, int32_t recip) {
   if (!segs || nseg < 1 || k < 1 || total_tiles < 0) return P2P_ERR_INVALID;
   if (total_tiles == 0) return P2P_OK;
-  hipLaunchKernelGGL(fedavg_segments_kernel, dim3(static_cast<unsigned>(total_tiles)), dim3(kBlock),
-                     0, static_cast<hipStream_t>(stream), segs, nseg, k, lr);
+  const dim3 grid(static_cast<unsigned>(total_tiles));
+  if (recip)
+    hipLaunchKernelGGL(fedavg_segments_kernel<true>, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), segs,
+                       nseg, k, lr);
+  else
+    hipLaunchKernelGGL(fedavg_segments_kernel<false>, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), segs,
+                       nseg, k, lr);
   return launch_status();
 }
 

@@ -17,17 +17,23 @@ import numpy as np
 import torch
 
 from . import _native as N
-from ._native import P2P_RULE_FEDAVG, P2P_RULE_MEDIAN, P2P_RULE_TRIMMED
+from ._native import P2P_RULE_FEDAVG, P2P_RULE_FEDAVG_TORCH_GPU, P2P_RULE_MEDIAN, P2P_RULE_TRIMMED
 
+# 'fedavg': the reference's ops as torch runs them on CPU tensors (true
+# division by K; the golden vectors).  'fedavg_torch_gpu': the same ops as
+# torch runs them on GPU tensors -- the reference's deployment, model on cuda
+# (node/node.py:28-29) -- where `acc /= K` is acc * fl(1/K) (include/p2pdl.h).
 RULES = {"fedavg": P2P_RULE_FEDAVG, "mean": P2P_RULE_FEDAVG, "median": P2P_RULE_MEDIAN,
-         "trimmed": P2P_RULE_TRIMMED, "trimmed_mean": P2P_RULE_TRIMMED}
+         "trimmed": P2P_RULE_TRIMMED, "trimmed_mean": P2P_RULE_TRIMMED,
+         "fedavg_torch_gpu": P2P_RULE_FEDAVG_TORCH_GPU}
+FEDAVG_RULES = (P2P_RULE_FEDAVG, P2P_RULE_FEDAVG_TORCH_GPU)
 MAX_ROBUST_PEERS = 256
 DEFAULT_TRIM_FRAC = 0.2
 
 
 def rule_id(rule) -> int:
     if isinstance(rule, int):
-        if rule not in (0, 1, 2):
+        if rule not in (0, 1, 2, 3):
             raise ValueError(f"unknown aggregation rule id {rule}")
         return rule
     try:
@@ -92,7 +98,7 @@ def aggregate(peers: Sequence[torch.Tensor], rule="fedavg", *, w: torch.Tensor |
     k = len(peers) if table is None else table.numel()
     if table is None:
         table = _peer_inputs(peers, n, ref.device)
-    if r != P2P_RULE_FEDAVG and k > MAX_ROBUST_PEERS:
+    if r not in FEDAVG_RULES and k > MAX_ROBUST_PEERS:
         raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {k}")
     b = 0
     if r == P2P_RULE_TRIMMED:
@@ -215,7 +221,7 @@ def _launch_table(base: int, L: int, tiles: int, K: int, r: int, b: int, lr: flo
 
 def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_frac, outs, dev, cache_key=None):
     r = rule_id(rule)
-    if r != P2P_RULE_FEDAVG and K > MAX_ROBUST_PEERS:
+    if r not in FEDAVG_RULES and K > MAX_ROBUST_PEERS:
         raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {K}")
     b = trim_count(K, trim_frac) if (r == P2P_RULE_TRIMMED and trim_b is None) else int(trim_b or 0)
     tile = int(N.lib().p2p_tile_elems(r, K))
