@@ -475,7 +475,7 @@ def test_device_inbox_digest_overlapped_with_landing(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rule", ["fedavg", "median", "trimmed"])
+@pytest.mark.parametrize("rule", ["fedavg", "median", "trimmed", "fedavg_torch_gpu"])
 def test_landed_updates_take_the_slab_fast_path(cuda, rule, monkeypatch):
     """aggregate_models on DeviceInbox-landed updates builds its kernel table
     from (slab, rows, key offsets) -- no per-tensor work -- and gives the same
@@ -493,8 +493,8 @@ def test_landed_updates_take_the_slab_fast_path(cuda, rule, monkeypatch):
     n = sum(int(np.prod(s)) for _, s in MLP_SHAPES)
     w = oracle.synth(n, 5, 0xFFFFF, 5e-2)
     flat = [np.concatenate([pickle.loads(s)[name].numpy().reshape(-1) for name, _ in MLP_SHAPES]) for s in ser]
-    if rule == "fedavg":
-        want, _ = oracle.fedavg(flat, w)
+    if rule in ("fedavg", "fedavg_torch_gpu"):
+        want, _ = oracle.fedavg(flat, w, torch_gpu=rule == "fedavg_torch_gpu")
     else:
         r = ops.rule_id(rule)
         want, _ = oracle.robust(flat, r, ops.trim_count(k) if r == 2 else 0, w=w)
