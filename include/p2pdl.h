@@ -20,7 +20,8 @@
  *     No exception ever crosses the ABI.
  *   - Numerics are bit-exact to the reference CPU op sequence:
  *     +0 accumulator init, fixed peer order, IEEE true division by K, and
- *     w + lr*agg with the multiply and the add separately rounded (no FMA).
+ *     w + lr*agg with the multiply and the add separately rounded (no FMA);
+ *     P2P_RULE_FEDAVG_TORCH_GPU divides as torch does on GPU tensors.
  */
 #ifndef P2PDL_H
 #define P2PDL_H
@@ -33,7 +34,8 @@ extern "C" {
 
 /* 2: p2p_set_robust_layout (a process-global A/B switch of version 1) is
  *    gone; every other entry point is unchanged.
- * 3: adds p2p_land_segments_f32 (K5, landing a received update). */
+ * 3: adds p2p_land_segments_f32 (K5, landing a received update).
+ * 4: adds the rule P2P_RULE_FEDAVG_TORCH_GPU (no signature changes). */
 #define P2P_ABI_VERSION 4
 
 typedef void *p2p_stream_t; /* hipStream_t */

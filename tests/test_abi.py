@@ -40,6 +40,9 @@ def test_abi_version_and_argument_errors_without_gpu():
     # per block; the trimmed mean's pair and LDS kernels share 64
     assert L.p2p_tile_elems(1, 129) == 128 and L.p2p_tile_elems(1, 256) == 128
     assert L.p2p_tile_elems(2, 200) == 64 and L.p2p_tile_elems(2, 256) == 64
+    assert L.p2p_tile_elems(3, 3) == 4096 and L.p2p_tile_elems(3, 300) == 4096  # FedAvg, torch-GPU division
+    assert L.p2p_aggregate_f32(1, 3, 0, 4, 0, 0.1, 16, None, None) == -1  # no rule 4
+    assert L.p2p_aggregate_segments_f32(1, 1, 0, 3, 4, 0, 0.1, None) == -1
     # argument validation happens before any HIP call
     assert L.p2p_fedavg_apply_f32(None, 3, 10, None, 0.1, None) == N.lib().p2p_aggregate_f32(
         None, 1, 1, 0, 0, 0.1, None, None, None) == -1
