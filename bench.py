@@ -446,6 +446,36 @@ def _numel(shape):
     return out
 
 
+def reference_on_gpu(model, updates, K, steps, warmup):
+    """Seconds per call of the reference's aggregation loop (reference
+    aggregator/aggregation.py:15-38, restated op for op) on the GPU tensors
+    of `model` and the update dicts: what the deployed reference -- model on
+    cuda, node/node.py:28-29 -- costs on this box.  Modifies the model."""
+    received = [{"model": u} for u in updates]
+
+    def call():
+        accumulated_updates = {key: torch.zeros_like(param) for key, param in model.state_dict().items()}  # :15
+        for received_model in received:  # :25-28
+            local_update = received_model["model"]
+            for key in accumulated_updates:
+                accumulated_updates[key] += local_update[key]
+        for key in accumulated_updates:  # :31-32
+            accumulated_updates[key] /= K
+        learning_rate = 0.1
+        for key in model.state_dict():  # :36-38
+            model.state_dict()[key] += learning_rate * accumulated_updates[key]
+
+    with torch.no_grad():
+        for _ in range(max(warmup, 1)):
+            call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call()
+        torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
 def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
     """aggregate_models (reference aggregator/aggregation.py:7-46) on a fake
     Node, end to end: host segment table + one kernel launch per call.
@@ -535,6 +565,7 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
         updates = plain
         general_s = timed_calls()
         ev.clear()
+        ref_s = reference_on_gpu(model, plain, K, steps, warmup)
     finally:
         agg.broadcast_global_model_update = saved
     call_ms = sum(a.elapsed_time(b) for a, b in ev_fast) / len(ev_fast)
@@ -567,12 +598,18 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
         "workload": name.replace("-", "_"), "value": round(K * n * 4 / step_s / 1e9, 2), "unit": "GB/s",
         "ms_per_step": round(step_s * 1e3, 4), "us_per_call": round(step_s * 1e6, 1),
         "us_per_call_general_path": round(general_s * 1e6, 1), "steps": steps,
+        "reference_on_gpu": {"us_per_call": round(ref_s * 1e6, 1), "speedup": round(ref_s / step_s, 1),
+                             "what": "the reference's aggregate_models loop (aggregation.py:15-38) as a node "
+                                     "on this GPU runs it: torch ops on the cuda tensors, state_dict() "
+                                     "rebuilt per key at :37-38; same model and updates (plain dicts)"},
         "scaling": "weak", "dtype": "fp32",
         "config": {"workload": f"{name}: drop-in aggregate_models, {len(sizes)}-tensor state_dict "
                                f"({n:,} params) x {K} updates landed in a DeviceInbox slab, one "
                                f"segment-table launch per call",
                    "peers": K, "coords_per_gpu": n, "tensors": len(sizes), "parallelism": "single GPU",
-                   "us_per_call": round(step_s * 1e6, 1), "us_per_call_general_path": round(general_s * 1e6, 1)},
+                   "us_per_call": round(step_s * 1e6, 1), "us_per_call_general_path": round(general_s * 1e6, 1),
+                   "reference_on_gpu_us_per_call": round(ref_s * 1e6, 1),
+                   "speedup_vs_reference_on_gpu": round(ref_s / step_s, 1)},
         "roofline": roofline(4 * n * (K + 2), call_ms, traffic_for(name, n, K),
                              timing="HIP events around aggregate_models (table H2D + segment kernel), in a "
                                     "pass after the timed loops (value / us_per_call: host wall time, no events)",
@@ -1242,6 +1279,8 @@ def compact_sub(rec: dict) -> dict:
     if "ms_per_step" in rec:
         out["ms"] = rec["ms_per_step"]
     out.update({k: rec[k] for k in SUB_KEEP if k in rec})
+    if "reference_on_gpu" in rec:
+        out["reference_on_gpu"] = {a: b for a, b in rec["reference_on_gpu"].items() if a != "what"}
     roof = rec.get("roofline") or {}
     if roof:
         out["frac"] = roof.get("frac")
