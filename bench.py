@@ -137,6 +137,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="main line only")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-reference-gpu", action="store_true",
+                    help="skip timing the reference's torch ops on the GPU beside the product")
     return ap.parse_args()
 
 
@@ -283,6 +285,26 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = sum(a.elapsed_time(b) for a, b in kern) / len(kern)
+    ref_s = None
+    if rule == "fedavg" and world == 1 and not args.no_reference_gpu:
+        # the reference's aggregation loop (aggregator/aggregation.py:15-38) as a
+        # node on this GPU runs it: torch ops over the same resident updates
+        ws = w[0, :C]
+
+        def reference_step():
+            acc = torch.zeros_like(ws)  # :15
+            for p in range(K):  # :25-28
+                acc += slab[p, 0, :C]
+            acc /= K  # :31-32
+            ws.add_(0.1 * acc)  # :36-38 (`+=` on the state_dict tensor)
+
+        reference_step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(2):
+            reference_step()
+        torch.cuda.synchronize()
+        ref_s = (time.perf_counter() - t0) / 2
     del slab, w, w_full, tables
     torch.cuda.empty_cache()
     step_s = elapsed / steps
@@ -312,7 +334,9 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
                                + (" (cfg3 per-GPU tile; N=8 -> the 1B-coordinate job)" if name == "cfg3" else ""),
                    "rule": rule, "peers": K, "coords_per_gpu": n, "coords_total": n * world,
                    "parallelism": parallelism(c),
-                   "pct_hbm_peak_step": round(4 * n * (K + 2) / step_s / 1e9 / HBM_PEAK_GBS, 4)},
+                   "pct_hbm_peak_step": round(4 * n * (K + 2) / step_s / 1e9 / HBM_PEAK_GBS, 4)}
+                  | ({"reference_on_gpu_ms_per_step": round(ref_s * 1e3, 3),
+                      "speedup_vs_reference_on_gpu": round(ref_s / step_s, 2)} if ref_s else {}),
         "roofline": roofline(4 * C * (K + 2), kern_ms, traffic_for(name, C, K)),
         "cpu_baseline": cpu,
     }
@@ -565,7 +589,7 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
         updates = plain
         general_s = timed_calls()
         ev.clear()
-        ref_s = reference_on_gpu(model, plain, K, steps, warmup)
+        ref_s = None if args.no_reference_gpu else reference_on_gpu(model, plain, K, steps, warmup)
     finally:
         agg.broadcast_global_model_update = saved
     call_ms = sum(a.elapsed_time(b) for a, b in ev_fast) / len(ev_fast)
@@ -598,18 +622,19 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
         "workload": name.replace("-", "_"), "value": round(K * n * 4 / step_s / 1e9, 2), "unit": "GB/s",
         "ms_per_step": round(step_s * 1e3, 4), "us_per_call": round(step_s * 1e6, 1),
         "us_per_call_general_path": round(general_s * 1e6, 1), "steps": steps,
-        "reference_on_gpu": {"us_per_call": round(ref_s * 1e6, 1), "speedup": round(ref_s / step_s, 1),
-                             "what": "the reference's aggregate_models loop (aggregation.py:15-38) as a node "
-                                     "on this GPU runs it: torch ops on the cuda tensors, state_dict() "
-                                     "rebuilt per key at :37-38; same model and updates (plain dicts)"},
+        "reference_on_gpu": None if ref_s is None else {
+            "us_per_call": round(ref_s * 1e6, 1), "speedup": round(ref_s / step_s, 1),
+            "what": "the reference's aggregate_models loop (aggregation.py:15-38) as a node on this GPU runs "
+                    "it: torch ops on the cuda tensors, state_dict() rebuilt per key at :37-38; same model "
+                    "and updates (plain dicts)"},
         "scaling": "weak", "dtype": "fp32",
         "config": {"workload": f"{name}: drop-in aggregate_models, {len(sizes)}-tensor state_dict "
                                f"({n:,} params) x {K} updates landed in a DeviceInbox slab, one "
                                f"segment-table launch per call",
                    "peers": K, "coords_per_gpu": n, "tensors": len(sizes), "parallelism": "single GPU",
-                   "us_per_call": round(step_s * 1e6, 1), "us_per_call_general_path": round(general_s * 1e6, 1),
-                   "reference_on_gpu_us_per_call": round(ref_s * 1e6, 1),
-                   "speedup_vs_reference_on_gpu": round(ref_s / step_s, 1)},
+                   "us_per_call": round(step_s * 1e6, 1), "us_per_call_general_path": round(general_s * 1e6, 1)}
+                  | ({"reference_on_gpu_us_per_call": round(ref_s * 1e6, 1),
+                      "speedup_vs_reference_on_gpu": round(ref_s / step_s, 1)} if ref_s else {}),
         "roofline": roofline(4 * n * (K + 2), call_ms, traffic_for(name, n, K),
                              timing="HIP events around aggregate_models (table H2D + segment kernel), in a "
                                     "pass after the timed loops (value / us_per_call: host wall time, no events)",
@@ -905,6 +930,16 @@ def run_delta_workload(args, n, seed, dev):
     step_s = (time.perf_counter() - t0) / args.steps
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     alg = 16 * n
+    ref_s = None
+    if not args.no_reference_gpu:  # the reference's ops on this GPU: a sub and a clone (node.py:279,282)
+        for i in range(3):
+            if i == 1:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            d, c = cur - prev, cur.clone()
+        torch.cuda.synchronize()
+        ref_s = (time.perf_counter() - t0) / 2
+        del d, c
     cpu = None
     if not args.no_cpu_baseline:
         import oracle.cpu_baseline as cb  # baseline leg only
@@ -920,7 +955,9 @@ def run_delta_workload(args, n, seed, dev):
         "ms_per_step": round(step_s * 1e3, 4), "scaling": "weak", "dtype": "fp32",
         "data": "synthetic (device counter PRNG); value = algorithmic bytes (16 B/param) per second",
         "config": {"workload": f"delta: trainer local update over {n:,} fp32 params (SURVEY §8(f) row 2)",
-                   "coords_per_gpu": n, "parallelism": "single GPU (replicas only)"},
+                   "coords_per_gpu": n, "parallelism": "single GPU (replicas only)"}
+                  | ({"reference_on_gpu_ms_per_step": round(ref_s * 1e3, 3),
+                      "speedup_vs_reference_on_gpu": round(ref_s / step_s, 2)} if ref_s else {}),
         "roofline": dict(roofline(alg, kern_ms, None), traffic=traffic_for("delta", n, 1)),
         "cpu_baseline": cpu}
 
@@ -1279,7 +1316,7 @@ def compact_sub(rec: dict) -> dict:
     if "ms_per_step" in rec:
         out["ms"] = rec["ms_per_step"]
     out.update({k: rec[k] for k in SUB_KEEP if k in rec})
-    if "reference_on_gpu" in rec:
+    if rec.get("reference_on_gpu"):
         out["reference_on_gpu"] = {a: b for a, b in rec["reference_on_gpu"].items() if a != "what"}
     roof = rec.get("roofline") or {}
     if roof:
@@ -1290,7 +1327,7 @@ def compact_sub(rec: dict) -> dict:
             out["traffic_x"] = round(tr / alg, 5)
     cfg = rec.get("config") or {}
     for k in ("reference_ms", "staging_ms", "pinned_digest_overlapped_ms", "with_digest", "hashes_product",
-              "speedup_vs_reference", "joined_ms"):
+              "speedup_vs_reference", "joined_ms", "reference_on_gpu_ms_per_step", "speedup_vs_reference_on_gpu"):
         if k in cfg:
             v = cfg[k]
             out[k] = {a: b for a, b in v.items() if a != "what"} if isinstance(v, dict) else v
