@@ -1,0 +1,102 @@
+"""The C ABI's calls are stream-ordered, allocate nothing and keep no state
+(include/p2pdl.h), so they can be captured into a HIP graph and replayed
+(INTEGRATION.md §2): captured once, replayed three times, every kernel
+family gives the bits of three eager calls -- FedAvg (reference
+aggregator/aggregation.py:15-38), the robust rules at K = 64 / 128 / 256 and
+the trainer delta (node/node.py:273-282)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+
+def _dev(a, cuda):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(cuda)
+
+
+@pytest.mark.gpu
+def test_fedavg_graph_replay_equals_repeated_calls(cuda):
+    from p2pdl_amd import ops
+
+    k, n = 5, 100_003
+    peers = [oracle.synth(n, 31, p, 1e-2) for p in range(k)]
+    w0 = oracle.synth(n, 31, 0xFFFFF, 5e-2)
+    pd = [_dev(p, cuda) for p in peers]
+    table = ops.pointer_table(pd, cuda)  # device table built before the capture
+    w = _dev(w0, cuda)
+    ops.aggregate(None, "fedavg", w=w, lr=0.1, table=table)  # warm-up
+    torch.cuda.synchronize()
+    w.copy_(_dev(w0, cuda))
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(cuda)
+    s.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            ops.aggregate(None, "fedavg", w=w, lr=0.1, table=table)
+    torch.cuda.synchronize()
+    assert np.array_equal(w.cpu().numpy().view(np.uint32), w0.view(np.uint32)), "capture must not execute"
+    want = w0
+    for _ in range(3):
+        g.replay()
+        want, _ = oracle.fedavg(peers, want)
+    torch.cuda.synchronize()
+    assert np.array_equal(w.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule,k", [("median", 64), ("trimmed", 128), ("median", 256), ("trimmed", 256)])
+def test_robust_graph_replay(cuda, rule, k):
+    from p2pdl_amd import ops
+
+    n = 20_011
+    peers = [oracle.synth(n, 37, p, 1e-2) for p in range(k)]
+    w0 = oracle.synth(n, 37, 0xFFFFF, 5e-2)
+    keep = [_dev(p, cuda) for p in peers]  # the table's targets stay alive
+    table = ops.pointer_table(keep, cuda)
+    w = _dev(w0, cuda)
+    ops.aggregate(None, rule, w=w, lr=0.1, table=table)  # warm-up
+    torch.cuda.synchronize()
+    w.copy_(_dev(w0, cuda))
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(cuda)
+    s.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            ops.aggregate(None, rule, w=w, lr=0.1, table=table)
+    rid = ops.rule_id(rule)
+    b = ops.trim_count(k) if rid == 2 else 0
+    want = w0
+    for _ in range(3):
+        g.replay()
+        want, _ = oracle.robust(peers, rid, b, w=want)
+    torch.cuda.synchronize()
+    assert np.array_equal(w.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_delta_graph_replay(cuda):
+    """Two replays of one captured delta launch: prev follows cur, delta is
+    cur - prev of the previous replay (0 after the first)."""
+    from p2pdl_amd import ops
+
+    n = 70_001
+    c0, p0 = oracle.synth(n, 41, 1, 1e-1), oracle.synth(n, 41, 2, 1e-1)
+    cur, prev = _dev(c0, cuda), _dev(p0, cuda)
+    delta = torch.empty_like(cur)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(cuda)
+    s.wait_stream(torch.cuda.current_stream(cuda))
+    ops.delta_snapshot_(cur, torch.empty_like(cur), delta, first=True)  # warm-up (other buffers)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            ops.delta_snapshot_(cur, prev, delta)
+    g.replay()
+    torch.cuda.synchronize()
+    want, _ = oracle.delta_snapshot_np(c0, p0)
+    assert np.array_equal(delta.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    assert torch.equal(prev, cur)
+    g.replay()
+    torch.cuda.synchronize()
+    assert not delta.cpu().numpy().view(np.uint32).any()  # x - x = +0 for every finite x
