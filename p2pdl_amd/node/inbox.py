@@ -753,7 +753,7 @@ class DeviceInbox:
         self.pool_bytes = int(pool_bytes if pool_bytes is not None else 2 * self.k_max * self.max_message_bytes)
         self._pinned_free = []     # _PinnedBuffer pool
         self._returned = deque()   # buffers of finalised handles, pooled at the next hand-out
-        self._consumers = {}       # stream handle -> event after its last kernel over the slab
+        self._consumers = {}       # stream handle -> (stream, event): streams whose kernels read the slab
         self._digests = {}
         self.count = 0
         # land() is called from the listener threads (one per connection,
@@ -873,23 +873,28 @@ class DeviceInbox:
         stream of the slab's device) reads slab rows: every later ``land``
         makes its own stream wait for that kernel before it overwrites a row
         (aggregation.py calls this after each launch over landed updates).
-        One event per consuming stream, re-recorded on raw handles -- no
-        allocation and no Stream object per call."""
+        The wait is set up by ``land``, not here: a land on another stream
+        records an event on each consuming stream at that moment -- after
+        every kernel issued on it so far -- and waits for it; a land on the
+        consuming stream itself is ordered by the stream.  So the per-call
+        cost of an aggregation is one dict lookup (a hipEventRecord per call
+        measured ~4.7 us of cfg1's ~14 us call, tools/prof_cfg1_parts.py)."""
         from .. import _native as N
 
         raw = stream.cuda_stream if stream is not None else N.stream_handle(self.device)
-        ev = self._consumers.get(raw)
-        if ev is not None:
-            N.event_record(ev.cuda_event, raw)
+        if raw in self._consumers:
             return
         with self._lock:
-            ev = torch.cuda.Event()
-            ev.record(stream or torch.cuda.current_stream(self.device))
-            self._consumers[raw] = ev
+            if raw not in self._consumers:
+                self._consumers[raw] = (stream or torch.cuda.current_stream(self.device), torch.cuda.Event())
 
     def _wait_rows_free(self, stream) -> None:
-        for ev in self._consumers.values():  # under self._lock
-            stream.wait_event(ev)
+        """Make ``stream`` wait for every kernel issued so far on the
+        streams that read the slab (under self._lock)."""
+        for raw, (consumer, ev) in self._consumers.items():
+            if raw != stream.cuda_stream:
+                ev.record(consumer)
+                stream.wait_event(ev)
 
     def order_after_landing(self, stream=None) -> None:
         """Make ``stream`` (default: the current stream of the slab's device)
