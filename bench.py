@@ -738,11 +738,13 @@ def run_digest_workload(args, rule, K, n, seed, dev):
     acc = K - len(bad)
     agg_bytes = 4 * n * (acc + 2) if rule == "fused" else 0
     cpu = None
+    sha_host = None  # this box's hashlib rate on the host threads: the host route's ceiling
     if not args.no_cpu_baseline:
         import oracle.cpu_baseline as cb  # baseline leg only
 
         sample = [bytes(buf[offsets[p]:offsets[p] + min(msg_bytes, 16 << 20)].cpu().numpy()) for p in range(min(K, 64))]
         res = cb.sha256(sample, args.cpu_seconds)
+        sha_host = res["value"]
         what = (f"hashlib.sha256 (OpenSSL, the function behind reference utils/crypto.py:56) over "
                 f"{len(sample)} x {len(sample[0]):,} B")
         if rule == "fused":
@@ -774,7 +776,11 @@ def run_digest_workload(args, rule, K, n, seed, dev):
                      "gpu_kernel_gbs": round(hashed / (gpu_kernel_ms / 1e3) / 1e9, 2),
                      # serial-chain issue bound: one wave issues ~1 instruction / 4 cycles at
                      # 2.4 GHz, ~910 instructions per 64-B block on the chain
-                     "chain_issue_bound_gbs": round(min(K, 65536) * 64 / (910 * 4 / 2.4e9) / 1e9, 2)},
+                     "chain_issue_bound_gbs": round(min(K, 65536) * 64 / (910 * 4 / 2.4e9) / 1e9, 2)}
+                    | ({  # the host route's own ceiling: this box's hashlib rate on the same threads
+                        "host_sha_bound_gbs": round(sha_host, 2),
+                        "frac_of_host_sha_bound": round(hashed / step_s / 1e9 / sha_host, 3)}
+                       if host_route and sha_host else {}),
         "cpu_baseline": cpu,
     }
 
@@ -1305,7 +1311,8 @@ def replica_workload(args, name, dev):
 
 # ------------------------------------------------------------------ main
 SUB_KEEP = ("us_per_call", "us_per_call_general_path", "ms_per_job", "kernel_ms_sum", "allgather_ms_sum")
-ROOF_KEEP = ("kernel_ms", "vs_flat_kernel", "fedavg_ms", "chain_issue_bound_gbs", "digest_route", "gpu_kernel_gbs")
+ROOF_KEEP = ("kernel_ms", "vs_flat_kernel", "fedavg_ms", "chain_issue_bound_gbs", "digest_route", "gpu_kernel_gbs",
+             "frac_of_host_sha_bound")
 
 
 def compact_sub(rec: dict) -> dict:
