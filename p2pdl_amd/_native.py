@@ -104,26 +104,6 @@ def require_device(t) -> None:
         raise RuntimeError(f"p2pdl_amd: tensors must be on a ROCm device, got {t.device}")
 
 
-_event_record = None
-
-
-def event_record(event_handle: int, stream_handle: int) -> None:
-    """hipEventRecord on raw handles (an existing torch.cuda.Event's
-    ``cuda_event``, a stream's ``cuda_stream``): ~0.5 us against ~4 us for
-    Event.record(torch.cuda.current_stream()).  Resolved through this
-    library's own dependency on the HIP runtime (dlsym searches the
-    library's dependency tree), i.e. the runtime torch uses."""
-    global _event_record
-    if _event_record is None:
-        fn = lib().hipEventRecord
-        fn.argtypes = [_P, _P]
-        fn.restype = _I32
-        _event_record = fn
-    rc = _event_record(event_handle, stream_handle)
-    if rc != 0:
-        raise P2PError(f"hipEventRecord failed ({rc})")
-
-
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = lib().p2p_strerror(rc)
