@@ -144,3 +144,47 @@ def test_misaligned_views_take_the_element_path(cuda, shift):
     torch.cuda.synchronize()
     want = oracle.fedavg(peers, w, torch_gpu=True)[0]
     assert np.array_equal(wt.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [3, 7, 64])
+def test_special_values_match_torch_on_the_gpu(cuda, K):
+    """±0, subnormals, ±inf, NaN and overflow through the reference's ops run
+    by torch on the GPU, against the kernel's fedavg_torch_gpu rule and the
+    oracle: subnormal inputs, quotients and products are kept (no flush to
+    zero on either side), NaN compared as a class."""
+    from p2pdl_amd import ops
+
+    rng = np.random.default_rng(7 + K)
+    tiny = np.array([0.0, -0.0, 1e-45, -1e-45, 1.17e-38, -3e-39, 2e-39, 5e-39, -7e-40], dtype=np.float32)
+    sp = np.array([np.inf, -np.inf, np.nan, 3.4e38, -3.4e38, 1.0, -1.0, 1e-7, 0.1, 1 / 3, 5e-38], dtype=np.float32)
+    n = 4099
+
+    def draw():  # mostly zeros and subnormals, specials at ~1 in 300 positions
+        x = rng.choice(tiny, size=n).astype(np.float32)
+        hit = rng.random(n) < 1 / 300
+        x[hit] = rng.choice(sp, size=int(hit.sum()))
+        return x
+
+    peers = [draw() for _ in range(K)]
+    w0 = draw()
+    # the reference's loop (aggregation.py:15-38) in torch on the GPU
+    acc = torch.zeros(n, device=cuda)
+    for p in peers:
+        acc += torch.from_numpy(p).to(cuda)
+    acc /= K
+    wt_ref = torch.from_numpy(w0.copy()).to(cuda)
+    wt_ref += 0.1 * acc
+    live = wt_ref.cpu().numpy()
+    want = oracle.fedavg(peers, w0, torch_gpu=True)[0]
+    wt = torch.from_numpy(w0.copy()).to(cuda)
+    ops.aggregate([torch.from_numpy(p).to(cuda) for p in peers], "fedavg_torch_gpu", w=wt, lr=0.1)
+    got = wt.cpu().numpy()
+
+    def same(a, b):
+        nan = np.isnan(a) & np.isnan(b)
+        return bool(np.all(nan | (a.view(np.uint32) == b.view(np.uint32))))
+
+    assert same(live, want), "torch on the GPU vs the oracle"
+    assert same(got, live), "kernel vs torch on the GPU"
+    assert np.any((np.abs(live) < 1.18e-38) & (live != 0)), "the case holds subnormal results"
