@@ -35,7 +35,8 @@ extern "C" {
 /* 2: p2p_set_robust_layout (a process-global A/B switch of version 1) is
  *    gone; every other entry point is unchanged.
  * 3: adds p2p_land_segments_f32 (K5, landing a received update).
- * 4: adds the rule P2P_RULE_FEDAVG_TORCH_GPU (no signature changes). */
+ * 4: adds the rule P2P_RULE_FEDAVG_TORCH_GPU and p2p_fedavg_apply_16
+ *    (float16 / bfloat16 models). */
 #define P2P_ABI_VERSION 4
 
 typedef void *p2p_stream_t; /* hipStream_t */
@@ -115,6 +116,16 @@ int32_t p2p_aggregate_f32(const float *const *peers, int32_t k, int64_t n, int32
 int32_t p2p_aggregate_segments_f32(const p2p_segment_t *segs, int32_t nseg, int64_t total_tiles,
                                    int32_t k, int32_t rule, int32_t trim_b, float lr,
                                    p2p_stream_t stream);
+
+/* FedAvg + apply on a float16 / bfloat16 model (aggregation.py:15-38 on a
+ * half-precision state_dict): peers / w hold the 16-bit storage of `dtype`
+ * (P2P_DTYPE_F16 or P2P_DTYPE_BF16); every op computed in fp32 and rounded
+ * to the storage type, as torch runs the reference's ops -- acc = r(acc + u)
+ * per update in list order, r(acc / K) (P2P_RULE_FEDAVG) or r(acc * fl(1/K))
+ * (P2P_RULE_FEDAVG_TORCH_GPU), w = r(w + r(lr * acc)). */
+enum { P2P_DTYPE_F16 = 1, P2P_DTYPE_BF16 = 2 };
+int32_t p2p_fedavg_apply_16(const uint16_t *const *peers, int32_t k, int64_t n, uint16_t *w, float lr,
+                            int32_t dtype, int32_t rule, p2p_stream_t stream);
 
 /* w += lr * agg, multiply and add separately rounded (aggregation.py:36-38). */
 int32_t p2p_apply_f32(float *w, const float *agg, float lr, int64_t n, p2p_stream_t stream);

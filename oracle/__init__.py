@@ -144,6 +144,59 @@ def fedavg_np(peers, w=None, lr: float = 0.1, torch_gpu: bool = False):
     return (np.asarray(w, dtype=np.float32) + np.float32(lr) * acc).astype(np.float32), acc
 
 
+# ------------------------------------------------- 16-bit models (a1-a4)
+def to_f32_16(bits, dtype: str) -> np.ndarray:
+    """uint16 storage bits of float16 / bfloat16 values -> exact float32."""
+    b = np.asarray(bits, dtype=np.uint16)
+    if dtype == "float16":
+        return b.view(np.float16).astype(np.float32)
+    return (b.astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+def round_16(x, dtype: str) -> np.ndarray:
+    """float32 -> uint16 bits, round to nearest even, as torch converts
+    (c10::Half / c10::BFloat16 from float; a NaN stays a NaN)."""
+    x = np.asarray(x, dtype=np.float32)
+    if dtype == "float16":
+        with np.errstate(over="ignore"):  # out of range -> +-inf, as torch converts
+            return x.astype(np.float16).view(np.uint16)
+    u = x.view(np.uint32).astype(np.uint64)
+    r = ((u + np.uint64(0x7FFF) + ((u >> np.uint64(16)) & np.uint64(1))) >> np.uint64(16)).astype(np.uint16)
+    return np.where(np.isnan(x), np.uint16(0x7FC0), r).astype(np.uint16)
+
+
+def round_16_once(x, dtype: str) -> np.ndarray:
+    """float64 -> float16 bits with ONE rounding (round to nearest even from
+    the exact value): round-to-odd to float32 first (24 >= 11 + 2 bits keeps
+    the single rounding exact), then float32 -> float16."""
+    assert dtype == "float16"
+    x = np.asarray(x, dtype=np.float64)
+    f = x.astype(np.float32)
+    away = np.abs(f.astype(np.float64)) > np.abs(x)
+    f = np.where(away, np.nextafter(f, np.float32(0)), f).astype(np.float32)
+    inexact = f.astype(np.float64) != x
+    b = f.view(np.uint32) | np.where(inexact & np.isfinite(x), np.uint32(1), np.uint32(0))
+    return round_16(b.astype(np.uint32).view(np.float32), dtype)
+
+
+def fedavg16_np(peers, w, dtype: str, lr: float = 0.1, torch_gpu: bool = False):
+    """The reference's ops (aggregation.py:15-38) on a float16 / bfloat16
+    model, as torch runs them: every op computed in float32 and rounded to
+    the storage type -- acc = +0 (:15); acc = r(acc + u) per update in list
+    order (:25-28); acc = r(acc / K) (:31-32; torch_gpu: r(acc * fl(1/K)),
+    ATen's division by a CPU scalar on a GPU tensor); t = r(fp32(lr) * acc);
+    w = r(w + t) (:36-38).  peers / w / result: uint16 bit arrays."""
+    f = lambda b: to_f32_16(b, dtype)
+    with np.errstate(over="ignore", invalid="ignore"):  # inf / NaN arithmetic is part of the contract
+        acc = np.zeros_like(f(w))
+        for p in peers:
+            acc = f(round_16(acc + f(p), dtype))
+        k = np.float32(len(peers))
+        acc = f(round_16(acc * (np.float32(1.0) / k) if torch_gpu else acc / k, dtype))
+        t = f(round_16(np.float32(lr) * acc, dtype))
+        return round_16(f(w) + t, dtype)
+
+
 # ---------------------------------------------------------------- robust rules
 def trim_count(k: int, trim_frac: float = 0.2) -> int:
     """b = floor(trim_frac * K), computed in exact integers

@@ -68,6 +68,12 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
     # keys and tensors of self.model.state_dict() (:15,:27,:37), from a cache
     # re-validated against the model on every call (model_state.py)
     keys, ws, st = model_state(self.model)
+    if ws and ws[0].dtype in ops.DTYPES_16:  # a float16 / bfloat16 model (e.g. model.half())
+        _aggregate_16(keys, ws, received, rule or AGGREGATION_RULE, lr)
+        logging.info(f"[{self.addr}:{self.port}] Model aggregation completed, applied local updates.")
+        self.received_models.clear()
+        broadcast_global_model_update(self)
+        return
     if _slab_fast_path(st, keys, ws, received, rule or AGGREGATION_RULE, lr, trim_frac):
         logging.info(f"[{self.addr}:{self.port}] Model aggregation completed, applied local updates.")
         self.received_models.clear()
@@ -136,20 +142,65 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
     broadcast_global_model_update(self)
 
 
+def _aggregate_16(keys, ws, received, rule, lr) -> None:
+    """A float16 / bfloat16 model: every op of :15-38 in fp32, rounded to the
+    storage type, as torch runs them (ops.fedavg16_apply_, one launch per
+    tensor).  Everything is checked before the first launch: a missing key
+    raises KeyError (:28), an integer tensor the reference's RuntimeError
+    (:32); a model mixing dtypes, updates of another dtype or a robust rule
+    raise NotImplementedError."""
+    _check_integers(keys, ws)
+    dt = ws[0].dtype
+    for key, t in zip(keys, ws):
+        if t.dtype != dt:
+            raise NotImplementedError(f"p2pdl_amd aggregates float32 models or uniform float16 / bfloat16 ones; "
+                                      f"{key} is {t.dtype}, {keys[0]} {dt}")
+    if ops.rule_id(rule) not in ops.FEDAVG_RULES:
+        raise NotImplementedError(f"rule {rule!r} on a {dt} model: the robust rules aggregate float32 models")
+    updates = [[received_model["model"][key] for key in keys] for received_model in received]  # KeyError (:28)
+    columns = []
+    for key, w, col in zip(keys, ws, zip(*updates)):
+        peers = []
+        for j, u in enumerate(col):
+            if u.dtype != dt:
+                raise NotImplementedError(f"update {j}, {key}: {u.dtype} into a {dt} model")
+            if u.device != w.device:
+                raise RuntimeError(f"Expected all tensors to be on the same device, but found at least two "
+                                   f"devices, {w.device} and {u.device}!")
+            if u.shape != w.shape:
+                raise RuntimeError(f"update {j}, {key}: shape {tuple(u.shape)} != {tuple(w.shape)}")
+            peers.append(u if u.is_contiguous() else u.contiguous())
+        columns.append(peers)
+    for w, peers in zip(ws, columns):
+        wc = w if w.is_contiguous() else w.contiguous()
+        ops.fedavg16_apply_(wc, peers, rule, lr)
+        if wc is not w:
+            w.copy_(wc)
+    _mark_rows_consumed(received)
+
+
+def _check_integers(keys, ws) -> None:
+    """The reference raises at the division for integer tensors (:32)."""
+    for t in ws:
+        if not t.is_floating_point():
+            name = _TORCH_TYPE_NAMES.get(t.dtype, str(t.dtype))
+            raise RuntimeError(f"result type Float can't be cast to the desired output type {name}")
+
+
 def _check_model(keys, ws, st) -> bool:
     """The reference raises at the division for integer tensors (:32);
-    float16 / float64 models are not aggregated here.  Returns whether every
+    a float32 model (16-bit ones take _aggregate_16; float64 and mixed
+    models are not aggregated here).  Returns whether every
     model tensor is contiguous.  Decided once per validated model-state
     entry (its tensors cannot change dtype or layout while it is valid)."""
     done = st.extra.get("checked") if st is not None else None
     if done is not None:
         return done
+    _check_integers(keys, ws)
     for key, t in zip(keys, ws):
-        if not t.is_floating_point():
-            name = _TORCH_TYPE_NAMES.get(t.dtype, str(t.dtype))
-            raise RuntimeError(f"result type Float can't be cast to the desired output type {name}")
         if t.dtype != torch.float32:
-            raise NotImplementedError(f"p2pdl_amd aggregates float32 state_dicts; {key} is {t.dtype}")
+            raise NotImplementedError(f"p2pdl_amd aggregates float32 models or uniform float16 / bfloat16 "
+                                      f"ones; {key} is {t.dtype}")
     contiguous = all(t.is_contiguous() for t in ws)
     if st is not None:
         st.extra["checked"] = contiguous

@@ -110,6 +110,34 @@ def aggregate(peers: Sequence[torch.Tensor], rule="fedavg", *, w: torch.Tensor |
                                           N.stream_handle()), "p2p_aggregate_f32")
 
 
+DTYPES_16 = {torch.float16: N.P2P_DTYPE_F16, torch.bfloat16: N.P2P_DTYPE_BF16}
+
+
+def fedavg16_apply_(w: torch.Tensor, peers: Sequence[torch.Tensor], rule="fedavg", lr: float = 0.1) -> None:
+    """FedAvg + apply in place on one float16 / bfloat16 tensor, every op
+    rounded to the storage type as torch runs the reference's ops
+    (aggregation.py:15-38; include/p2pdl.h p2p_fedavg_apply_16)."""
+    N.require_device(w)
+    dt = DTYPES_16.get(w.dtype)
+    if dt is None:
+        raise TypeError(f"w: expected float16 or bfloat16, got {w.dtype}")
+    if not w.is_contiguous():
+        raise ValueError("w: must be contiguous")
+    r = rule_id(rule)
+    if r not in FEDAVG_RULES:
+        raise NotImplementedError(f"rule {rule!r} on a {w.dtype} model: the robust rules aggregate float32 models")
+    if len(peers) == 0:
+        raise ValueError("need at least one peer update")
+    for i, p in enumerate(peers):
+        if p.dtype != w.dtype or p.device != w.device or not p.is_contiguous() or p.numel() != w.numel():
+            raise ValueError(f"peers[{i}]: expected a contiguous {w.dtype} tensor of {w.numel()} elements on "
+                             f"{w.device}, got {p.dtype} {p.numel()} on {p.device}")
+    table = pointer_table(peers, w.device)
+    with torch.cuda.device(w.device):
+        N.check(N.lib().p2p_fedavg_apply_16(table.data_ptr(), len(peers), w.numel(), w.data_ptr(), lr, dt, r,
+                                            N.stream_handle()), "p2p_fedavg_apply_16")
+
+
 def fedavg_apply_(w: torch.Tensor, peers: Sequence[torch.Tensor], lr: float = 0.1) -> torch.Tensor:
     """w += lr * mean(peers) in place (reference aggregation.py:15-38)."""
     aggregate(peers, "fedavg", w=w, lr=lr)
