@@ -9,8 +9,8 @@
 //   w   = r(w + r(fp32(lr) * acc))            (:36-38)
 // with r() round-to-nearest-even to float16 / bfloat16 (torch's conversions;
 // a NaN stays a NaN).  2(K+2) bytes per coordinate, HBM-bound like
-// the fp32 kernel; each lane handles 4 consecutive coordinates per step with
-// one 8-byte load per peer (one 512-B wave instruction).
+// the fp32 kernel; each lane handles 8 consecutive coordinates per step with
+// one 16-byte load per peer (one 1-KiB wave instruction), 4 peers in flight.
 #include "p2p_common.h"
 
 namespace p2p {
@@ -66,32 +66,46 @@ __device__ __forceinline__ uint16_t fedavg16_one(float acc, float fk, float inv,
   return f32_to_16<DT>(pin(__fadd_rn(f16_to_f32<DT>(w), t)));
 }
 
-typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+constexpr int kV16 = 8;       // coordinates per lane per step: one 16-byte load per peer (1 KiB per wave)
+constexpr int kU16 = 4;       // peer loads in flight per lane before the rounding chain consumes them
 
 template <int DT, bool RECIP>
 __global__ __launch_bounds__(kBlock) void fedavg16_kernel(const uint16_t* const* __restrict__ peers, int K,
                                                           int64_t n, uint16_t* w, float lr) {
-  uintptr_t a = reinterpret_cast<uintptr_t>(w);  // 8-byte vector loads need every buffer 8-byte aligned
+  uintptr_t a = reinterpret_cast<uintptr_t>(w);  // 16-byte vector loads need every buffer 16-byte aligned
   for (int k = 0; k < K; ++k) a |= reinterpret_cast<uintptr_t>(table_at(peers, k));
-  const bool vec = (a & 7) == 0;
+  const bool vec = (a & 15) == 0;
   const float fk = static_cast<float>(K);
   const float inv = RECIP ? 1.0f / fk : 0.f;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock * 4;
-  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4; i < n; i += stride) {
-    if (vec && i + 4 <= n) {
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < K; ++k) {
-        const u16x4 u = ldg(reinterpret_cast<const u16x4*>(table_at(peers, k) + i));
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock * kV16;
+  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * kV16; i < n; i += stride) {
+    if (vec && i + kV16 <= n) {
+      float acc[kV16];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] = rnd<DT>(__fadd_rn(acc[e], f16_to_f32<DT>(u[e])));
+      for (int e = 0; e < kV16; ++e) acc[e] = 0.f;
+      int k = 0;
+      for (; k + kU16 <= K; k += kU16) {
+        u16x8 u[kU16];
+#pragma unroll
+        for (int j = 0; j < kU16; ++j) u[j] = ldg_nt(reinterpret_cast<const u16x8*>(table_at(peers, k + j) + i));
+#pragma unroll
+        for (int j = 0; j < kU16; ++j)  // strictly in list order (:25-28)
+#pragma unroll
+          for (int e = 0; e < kV16; ++e) acc[e] = rnd<DT>(__fadd_rn(acc[e], f16_to_f32<DT>(u[j][e])));
       }
-      const u16x4 wv = ldg(reinterpret_cast<const u16x4*>(w + i));
-      u16x4 o;
+      for (; k < K; ++k) {
+        const u16x8 u = ldg_nt(reinterpret_cast<const u16x8*>(table_at(peers, k) + i));
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = fedavg16_one<DT, RECIP>(acc[e], fk, inv, lr, wv[e]);
-      stg(reinterpret_cast<u16x4*>(w + i), o);
+        for (int e = 0; e < kV16; ++e) acc[e] = rnd<DT>(__fadd_rn(acc[e], f16_to_f32<DT>(u[e])));
+      }
+      const u16x8 wv = ldg(reinterpret_cast<const u16x8*>(w + i));
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < kV16; ++e) o[e] = fedavg16_one<DT, RECIP>(acc[e], fk, inv, lr, wv[e]);
+      stg(reinterpret_cast<u16x8*>(w + i), o);
     } else {
-      for (int64_t j = i; j < n && j < i + 4; ++j) {
+      for (int64_t j = i; j < n && j < i + kV16; ++j) {
         float acc = 0.f;
         for (int k = 0; k < K; ++k) acc = rnd<DT>(__fadd_rn(acc, f16_to_f32<DT>(ldg(table_at(peers, k) + j))));
         stg(w + j, fedavg16_one<DT, RECIP>(acc, fk, inv, lr, ldg(w + j)));
@@ -111,7 +125,7 @@ extern "C" int32_t p2p_fedavg_apply_16(const uint16_t* const* peers, int32_t k, 
   if (rule != P2P_RULE_FEDAVG && rule != P2P_RULE_FEDAVG_TORCH_GPU) return P2P_ERR_INVALID;
   if (reinterpret_cast<uintptr_t>(w) & 1) return P2P_ERR_ALIGN;
   if (n == 0) return P2P_OK;
-  const int64_t groups = ceil_div(n, 4);
+  const int64_t groups = ceil_div(n, kV16);
   const int64_t blocks = ceil_div(groups, kBlock);
   const unsigned grid = static_cast<unsigned>(blocks < 256 * 8 ? blocks : 256 * 8);
   const hipStream_t s = static_cast<hipStream_t>(stream);
