@@ -25,6 +25,7 @@ Build extensions (keyword-only, defaults reproduce the reference): ``rule``
 GPU tensors -- its deployment, node/node.py:28-29 -- where :32 is
 acc * fl(1/K)), ``lr`` (:36) and ``trim_frac``.
 """
+import contextlib
 import logging
 import pickle
 import socket
@@ -34,15 +35,15 @@ import numpy as np
 import torch
 
 from .. import ops
+from .._native import host_extension
 from ..node import envelope
 from ..node.inbox import LandedUpdate
 from ..utils.waiting import wait_for_models
 from .model_state import model_state
 
-try:  # host-side C gather of the peer table (p2pdl_amd/csrc/host_tables.cpp)
-    from .. import _host_tables
-except ImportError:  # not built: the per-tensor Python path (same results)
-    _host_tables = None
+# host-side C gather of the peer table (p2pdl_amd/csrc/host_tables.cpp); no
+# silent fallback when it is not built (NativeUnavailable at import)
+_host_tables = host_extension("_host_tables")
 
 LEARNING_RATE = 0.1       # reference aggregation.py:36
 AGGREGATION_RULE = "fedavg"
@@ -93,17 +94,17 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
 
     if table is not None:
         if contiguous:  # the validated model-state entry vouches for the pointers
-            ops.aggregate_ptr_table_(ws, table, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac,
-                                     w_ptrs=st.ptrs if st is not None else None,
-                                     numels=st.numels if st is not None else None)
-            _mark_rows_consumed(received)
+            with _consuming(received):
+                ops.aggregate_ptr_table_(ws, table, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac,
+                                         w_ptrs=st.ptrs if st is not None else None,
+                                         numels=st.numels if st is not None else None)
             logging.info(f"[{self.addr}:{self.port}] Model aggregation completed, applied local updates.")
             self.received_models.clear()
             broadcast_global_model_update(self)
             return
         ws_c = [w if w.is_contiguous() else w.contiguous() for w in ws]
-        ops.aggregate_ptr_table_(ws_c, table, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac)
-        _mark_rows_consumed(received)
+        with _consuming(received):
+            ops.aggregate_ptr_table_(ws_c, table, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac)
         for w, wc in zip(ws, ws_c):
             if wc is not w:
                 w.copy_(wc)
@@ -127,8 +128,8 @@ def aggregate_models(self, *, rule=None, lr=LEARNING_RATE, trim_frac=TRIM_FRAC):
     # state_dict() tensors are views of the parameters: updating them in place
     # updates the model, exactly like the reference's `+=` at :38.
     ws_c = [w if w.is_contiguous() else w.contiguous() for w in ws]
-    ops.aggregate_segments_(ws_c, peer_lists, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac)
-    _mark_rows_consumed(received)
+    with _consuming(received):
+        ops.aggregate_segments_(ws_c, peer_lists, rule or AGGREGATION_RULE, lr=lr, trim_frac=trim_frac)
     for w, wc in zip(ws, ws_c):
         if wc is not w:
             w.copy_(wc)
@@ -173,10 +174,10 @@ def _aggregate_16(keys, ws, received, rule, lr) -> None:
         columns.append(peers)
     for w, peers in zip(ws, columns):
         wc = w if w.is_contiguous() else w.contiguous()
-        ops.fedavg16_apply_(wc, peers, rule, lr)
+        with _consuming(received):
+            ops.fedavg16_apply_(wc, peers, rule, lr)
         if wc is not w:
             w.copy_(wc)
-    _mark_rows_consumed(received)
 
 
 def _check_integers(keys, ws) -> None:
@@ -212,7 +213,7 @@ def _gather_table(received, keys, ws):
     when the C gather cannot vouch for every tensor (not fp32 / contiguous /
     on the model's CUDA device / the parameter's element count) -- the
     caller's per-tensor path then diagnoses or widens exactly as before."""
-    if _host_tables is None or not keys:
+    if not keys:
         return None
     dev = ws[0].device
     if dev.type != "cuda":
@@ -273,35 +274,39 @@ def _slab_fast_path(st, keys, ws, received, rule, lr, trim_frac) -> bool:
         offsets = tuple(offsets)
         if st is not None:
             st.extra["slab"] = (weakref.ref(inbox), offsets)
-    inbox.order_after_landing()  # land()'s row copies ran on the listener thread's stream
     rows = tuple(rm["model"].row for rm in received)
     # the launch itself is cached on the validated model-state entry: the same
     # rows, rule and trim as the last call over this inbox -> the same device
     # table, launched again with no per-call work (ops.relaunch)
     ck = (rows, rule, trim_frac)
     last = st.extra.get("launch") if st is not None else None
-    if last is not None and last[0] == ck and last[1]() is inbox:
-        ops.relaunch(last[2], inbox.slab.device, len(ws), len(rows), lr)
-    else:
-        entry = ops.aggregate_slab_rows_(ws, inbox.slab, rows, offsets, rule, lr=lr, trim_frac=trim_frac,
-                                         w_ptrs=st.ptrs if st is not None else None,
-                                         numels=st.numels if st is not None else None)
-        if st is not None and entry is not None:
-            st.extra["launch"] = (ck, weakref.ref(inbox), entry)
-    inbox.slab_consumed()  # the next round's land() into these rows waits for this kernel
+    # ordered after land()'s row copies (they ran on the listener threads'
+    # streams), and the next round's land() into these rows after this kernel
+    with inbox.consuming():
+        if last is not None and last[0] == ck and last[1]() is inbox:
+            ops.relaunch(last[2], inbox.slab.device, len(ws), len(rows), lr)
+        else:
+            entry = ops.aggregate_slab_rows_(ws, inbox.slab, rows, offsets, rule, lr=lr, trim_frac=trim_frac,
+                                             w_ptrs=st.ptrs if st is not None else None,
+                                             numels=st.numels if st is not None else None)
+            if st is not None and entry is not None:
+                st.extra["launch"] = (ck, weakref.ref(inbox), entry)
     return True
 
 
-def _mark_rows_consumed(received) -> None:
-    """General path over landed updates (e.g. mixed with plain dicts): each
-    inbox learns that the launch just issued reads its rows."""
+def _consuming(received):
+    """General path over landed updates (e.g. mixed with plain dicts): the
+    launch in this block is ordered after each inbox's landing copies and
+    registered with it before it is queued (DeviceInbox.consuming)."""
     inboxes = {}
     for rm in received:
         u = rm.get("model") if isinstance(rm, dict) else None
         if isinstance(u, LandedUpdate):
             inboxes[id(u.inbox)] = u.inbox
+    stack = contextlib.ExitStack()
     for inbox in inboxes.values():
-        inbox.slab_consumed()
+        stack.enter_context(inbox.consuming())
+    return stack
 
 
 def broadcast_global_model_update(self):

@@ -158,17 +158,145 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
     }
 }
 
-// Flat buffer, one tile per block.  K either from the kernarg or, when
-// k_dev != nullptr, from device memory (fused accept -> FedAvg path).
+// Flat buffer, one tile per block, tiles tile_base, tile_base + 1, ...  K
+// either from the kernarg or, when k_dev != nullptr, from device memory
+// (fused accept -> FedAvg path).
 template <int NV, bool RECIP>
 __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const* __restrict__ peers,
                                                              int K, const int32_t* k_dev,
                                                              int64_t n, float* w, float* out,
-                                                             float lr) {
+                                                             float lr, int64_t tile_base) {
   if (k_dev) K = *k_dev;
   if (K <= 0) return;
   const bool aligned = all_aligned16(peers, K, w, out);
-  fedavg_tile<NV, RECIP>(peers, K, n, static_cast<int64_t>(blockIdx.x) * tile_of<NV>(), w, out, lr, aligned);
+  fedavg_tile<NV, RECIP>(peers, K, n, (tile_base + static_cast<int64_t>(blockIdx.x)) * tile_of<NV>(), w, out, lr,
+                         aligned);
+}
+
+// ---------------------------------------------------------------------------
+// K1s (round 5): the same reduction with the peer streams staged by LDS-DMA
+// through DEDICATED loader waves (tools/fedavg_split.hip, profiles/r05/split*).
+//
+// A block = kSL loader waves + kSC consumer waves and owns tiles b, b + G, ...
+// of kSTile floats.  A stage is one peer's 32-KiB slice of one tile; the
+// block's stages run (tile, peer) in list order through a ring of kSS
+// stages in LDS (+ one slot for the tile's w).  Loaders issue
+// global_load_lds_dwordx4 nt (1 KiB per wave instruction, no VGPR
+// destination); one barrier per stage: before barrier i each loader waits
+// (vmcnt) for its part of stage i, after it refills the slot stage i-1 used
+// with stage i + kSS - 1, so 2-3 stages (64-96 KiB) are in flight per CU at
+// every moment -- more than one wave can hold (vmcnt is 6 bits: 63 KiB).
+// Consumer wave c owns floats [c * kSTile / kSC, (c + 1) * kSTile / kSC) of
+// the tile: ds_read_b128 of its part of stage i and the add, in peer order
+// from +0 (:15, :25-28); after the tile's last peer / K and the apply
+// (:31-38) exactly as fedavg_tile_vec -- the same per-coordinate op order,
+// so the bits are those of the VGPR kernel.  Measured against the VGPR
+// kernel, interleaved on one box: cfg3 tile (256 x 125M) +2-3%, 256 x 16M
+// +2-7% across three boxes; the loaders alone (no consumers) reach 6.4-7.0
+// TB/s with this access pattern.
+constexpr int kSL = 4;                       // loader waves
+constexpr int kSC = 8;                       // consumer waves
+constexpr int kSS = 4;                       // ring stages
+constexpr int kSTile = 8192;                 // floats per tile (32 KiB per peer)
+constexpr int kSPer = kSTile / 256 / kSL;    // DMA instructions per loader per stage
+constexpr int kSRpw = kSTile / 256 / kSC;    // ds_read_b128 per consumer lane per stage
+static_assert((kSS - 2) * kSPer <= 63, "vmcnt is 6 bits");
+static_assert(kSRpw == 4, "lds_read4");
+constexpr int64_t kSGridCap = 2048;          // 8 blocks per CU of 256 (one resident at a time)
+constexpr int kSplitMinK = 16;
+constexpr int64_t kSplitMinTiles = 2048;     // below: the tail of too few tiles per CU
+
+#define P2P_LDS __attribute__((address_space(3)))
+template <int AUX>
+__device__ __forceinline__ void dma16(const float* src, float* lds_dst) {
+  __builtin_amdgcn_global_load_lds((P2P_GLOBAL void*)(const_cast<float*>(src)), (P2P_LDS void*)lds_dst, 16, 0, AUX);
+}
+// Four ds_read_b128 of this lane's part at LDS byte address a, waited in the
+// same statement (hipcc neither counts nor reorders around it).
+__device__ __forceinline__ void lds_read4(f4 (&x)[4], uint32_t a) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
+      "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
+      : "v"(a));
+}
+
+template <bool RECIP>
+__global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const float* const* __restrict__ peers,
+                                                                        int K, const int32_t* k_dev,
+                                                                        int64_t ntiles, float* w, float* out,
+                                                                        float lr) {
+  __shared__ __attribute__((aligned(16))) float lds[(kSS + 1) * kSTile];
+  if (k_dev) K = __builtin_amdgcn_readfirstlane(ldg(k_dev));
+  if (K <= 0) return;
+  const int64_t G = gridDim.x, b = bid_x();
+  const int wv = __builtin_amdgcn_readfirstlane(tid_x() >> 6), lane = tid_x() & 63;
+  if (!all_aligned16(peers, K, w, out)) {
+    // 4-B-aligned views: element-wise, same op order, no LDS (block-uniform)
+    for (int64_t t = b; t < ntiles; t += G)
+      for (int e = tid_x(); e < kSTile; e += 64 * (kSL + kSC))
+        fedavg_elem<RECIP>(peers, K, t * kSTile + e, w, out, lr);
+    return;
+  }
+  const int64_t N = (ntiles - b + G - 1) / G * K;  // stages (= barriers) of this block
+  if (wv < kSL) {
+    int64_t ti = b, issued = 0;
+    int ki = 0, si = 0;
+    auto issue = [&]() {
+      const float* src = table_at(peers, ki) + ti * kSTile + (wv * kSPer) * 256 + lane * 4;
+#pragma unroll
+      for (int q = 0; q < kSPer; ++q) dma16<2 /* nt */>(src + q * 256, &lds[si * kSTile + (wv * kSPer + q) * 256]);
+      ++issued;
+      si = si + 1 == kSS ? 0 : si + 1;
+      if (++ki == K) { ki = 0; ti += G; }
+    };
+    for (int d = 0; d < kSS - 1 && issued < N; ++d) issue();
+    for (int64_t i = 0; i < N; ++i) {
+      if (i + kSS - 2 < N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kSS - 2) * kSPer) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // stage i landed; stage i-1's slot read
+      if (issued < N) issue();       // into that slot
+    }
+    return;
+  }
+  const int cw = wv - kSL;
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(&lds[0]));
+  const uint32_t mine = static_cast<uint32_t>(cw * kSRpw * 256 + lane * 4) * 4u;
+  const float fk = static_cast<float>(K);
+  const float inv = RECIP ? 1.0f / fk : 0.f;
+  int slot = 0;
+  for (int64_t t = b; t < ntiles; t += G) {
+    const int64_t o = t * kSTile + cw * kSRpw * 256 + lane * 4;
+    if (w) {
+#pragma unroll
+      for (int r = 0; r < kSRpw; ++r) dma16<0>(w + o + r * 256, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
+    }
+    f4 acc[kSRpw];
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
+    for (int k = 0; k < K; ++k) {
+      __builtin_amdgcn_s_barrier();
+      f4 x[kSRpw];
+      lds_read4(x, lds0 + static_cast<uint32_t>(slot) * (kSTile * 4) + mine);
+#pragma unroll
+      for (int r = 0; r < kSRpw; ++r) acc[r] += x[r];  // strictly in list order (:25-28)
+      slot = slot + 1 == kSS ? 0 : slot + 1;
+    }
+    f4 m[kSRpw];
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r) m[r] = div4<RECIP>(acc[r], fk, inv);  // (:31-32)
+    if (out) {
+#pragma unroll
+      for (int r = 0; r < kSRpw; ++r) st(out + o + r * 256, m[r]);
+    }
+    if (w) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w DMA (and its older stores)
+      f4 wq[kSRpw];
+      lds_read4(wq, lds0 + static_cast<uint32_t>(kSS * kSTile * 4) + mine);
+#pragma unroll
+      for (int r = 0; r < kSRpw; ++r) st(w + o + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
+    }
+  }
 }
 
 // Whole state_dict: one tile per block, segment found by binary search.
@@ -196,13 +324,33 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* ag
 
 static int grid_for_tiles(int64_t ntiles) { return static_cast<int>(ntiles > 0 ? ntiles : 1); }
 
+// Flat launches: the split kernel over the whole kSTile tiles of a large
+// buffer (K >= kSplitMinK, >= kSplitMinTiles tiles), the VGPR kernel over
+// the rest (the tail, or all of a smaller buffer).  K is the kernarg or, for
+// the device-K path, k_max.
 static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,
                         float lr, hipStream_t stream, bool recip = false) {
-  const dim3 grid(grid_for_tiles(ceil_div(n, kTile)));
+  const int64_t full = K >= kSplitMinK ? n / kSTile : 0;
+  int64_t done = 0;
+  if (full >= kSplitMinTiles) {
+    const dim3 grid(static_cast<unsigned>(full < kSGridCap ? full : kSGridCap));
+    const dim3 block(64 * (kSL + kSC));
+    if (recip)
+      hipLaunchKernelGGL(fedavg_split_kernel<true>, grid, block, 0, stream, peers, K, k_dev, full, w, out, lr);
+    else
+      hipLaunchKernelGGL(fedavg_split_kernel<false>, grid, block, 0, stream, peers, K, k_dev, full, w, out, lr);
+    done = full * kSTile;
+    if (done == n) return;
+  }
+  static_assert(kSTile % kTile == 0, "split tiles are whole VGPR tiles");
+  const int64_t tile_base = done / kTile;
+  const dim3 grid(grid_for_tiles(ceil_div(n - done, kTile)));
   if (recip)
-    hipLaunchKernelGGL((fedavg_flat_kernel<kNV, true>), grid, dim3(kBlock), 0, stream, peers, K, k_dev, n, w, out, lr);
+    hipLaunchKernelGGL((fedavg_flat_kernel<kNV, true>), grid, dim3(kBlock), 0, stream, peers, K, k_dev, n, w, out, lr,
+                       tile_base);
   else
-    hipLaunchKernelGGL((fedavg_flat_kernel<kNV, false>), grid, dim3(kBlock), 0, stream, peers, K, k_dev, n, w, out, lr);
+    hipLaunchKernelGGL((fedavg_flat_kernel<kNV, false>), grid, dim3(kBlock), 0, stream, peers, K, k_dev, n, w, out,
+                       lr, tile_base);
 }
 
 static int grid_stride_blocks(int64_t nblocks) {

@@ -130,8 +130,10 @@ struct Parser {
     return true;
   }
 
+  // bytes [p, p + k) exist; no signed overflow for any k (a peer's 8-byte
+  // length may be near INT64_MAX)
   void need(const Stream& st, int64_t p, int64_t k) const {
-    if (k < 0 || p < 0 || p + k > st.end) fail("truncated pickle");
+    if (k < 0 || p < 0 || p > st.end || k > st.end - p) fail("truncated pickle");
   }
   uint64_t le(const Stream& st, int64_t p, int k) const {
     need(st, p, k);
@@ -292,7 +294,7 @@ struct Parser {
     const std::string& t = stype->s;
     if (t == "FloatStorage" || t == "IntStorage") item = 4;
     else if (t == "DoubleStorage" || t == "LongStorage") item = 8;
-    else if (t == "HalfStorage" || t == "ShortStorage") item = 2;
+    else if (t == "HalfStorage" || t == "BFloat16Storage" || t == "ShortStorage") item = 2;
     else if (t == "CharStorage" || t == "ByteStorage" || t == "BoolStorage") item = 1;
     else fail(t + " is not supported");
     if (pos + 8 > st.end) fail("truncated storage blob");
@@ -469,7 +471,7 @@ struct Parser {
         }
         case 0x8E: {  // BINBYTES8
           const uint64_t k = le(st, pos, 8);
-          if (k > static_cast<uint64_t>(INT64_MAX)) fail("truncated pickle");
+          if (k > static_cast<uint64_t>(st.end - (pos + 8))) fail("truncated pickle");  // before any use of k
           stack.push_back(bytes_at(st, pos + 8, static_cast<int64_t>(k)));
           pos += 8 + static_cast<int64_t>(k);
           break;

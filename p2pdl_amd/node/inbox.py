@@ -35,6 +35,7 @@ this on torch-produced pickles of the reference's message shapes).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import pickle
@@ -46,6 +47,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
+from .._native import host_extension
 from ..utils import digests
 
 # torch legacy serialization (torch/serialization.py _legacy_save): magic
@@ -53,14 +55,17 @@ from ..utils import digests
 # (storages as persistent ids), the storage-key list pickle, then per key an
 # int64 element count and the raw bytes.
 _LEGACY_MAGIC = 0x1950A86A20F9469CFC6C
+# numpy has no bfloat16: a BFloat16Storage payload is held as its uint16 bit
+# patterns (no other storage type maps to uint16) and materialised as a
+# torch.bfloat16 view of them (RawTensor.tensor).
 _STORAGE_DTYPES = {
     "FloatStorage": np.float32, "DoubleStorage": np.float64, "HalfStorage": np.float16,
-    "BFloat16Storage": None, "LongStorage": np.int64, "IntStorage": np.int32, "ShortStorage": np.int16,
+    "BFloat16Storage": np.uint16, "LongStorage": np.int64, "IntStorage": np.int32, "ShortStorage": np.int16,
     "CharStorage": np.int8, "ByteStorage": np.uint8, "BoolStorage": np.bool_,
 }
 _TORCH_DTYPES = {np.float32: torch.float32, np.float64: torch.float64, np.float16: torch.float16,
-                 np.int64: torch.int64, np.int32: torch.int32, np.int16: torch.int16, np.int8: torch.int8,
-                 np.uint8: torch.uint8, np.bool_: torch.bool}
+                 np.uint16: torch.bfloat16, np.int64: torch.int64, np.int32: torch.int32, np.int16: torch.int16,
+                 np.int8: torch.int8, np.uint8: torch.uint8, np.bool_: torch.bool}
 
 
 @dataclass
@@ -90,6 +95,16 @@ class RawTensor:
         item = base.itemsize
         return np.lib.stride_tricks.as_strided(base[self.offset:], shape=self.size,
                                                strides=tuple(s * item for s in self.stride), writeable=False)
+
+    def tensor(self, device=None) -> torch.Tensor:
+        """A torch tensor holding a copy of the payload, of the storage's
+        dtype (bfloat16 from its bit patterns), on ``device`` (default: the
+        storage's own location, as ``pickle.loads`` restores it)."""
+        t = torch.from_numpy(np.array(self.array()))
+        if self.storage.dtype is np.uint16:
+            t = t.view(torch.bfloat16)
+        dev = self.storage.location if device is None else device
+        return t if str(dev) == "cpu" else t.to(dev)
 
 
 class _Mark:
@@ -355,8 +370,6 @@ def parse_legacy_storage(blob) -> RawStorage:
     if keys != [key]:
         raise pickle.UnpicklingError("expected exactly one storage per blob")
     dt = _STORAGE_DTYPES[stype]
-    if dt is None:
-        raise pickle.UnpicklingError(f"{stype} is not supported")
     if pos + 8 > len(mv):
         raise pickle.UnpicklingError("truncated storage blob")
     (count,) = struct.unpack_from("<q", mv, pos)
@@ -429,10 +442,11 @@ def _is_tensor_dict(obj) -> bool:
     return isinstance(obj, dict) and all(isinstance(v, RawTensor) for v in dict.values(obj))
 
 
-try:  # the same machine in C++ (csrc/wire.cpp), built beside the HIP library
-    from .. import _wire
-except ImportError:
-    _wire = None
+# the same machine in C++ (csrc/wire.cpp), built beside the HIP library; the
+# product parses with it (NativeUnavailable at import when it is not built).
+# The Python machine above stays as its differential reference in the tests
+# (ZeroCopyParser(native=False)).
+_wire = host_extension("_wire")
 
 
 class ZeroCopyParser:
@@ -444,16 +458,14 @@ class ZeroCopyParser:
     ``pickle.UnpicklingError`` (so a listener that catches only that cannot
     be killed by a peer's bytes).
 
-    ``native`` (default: when built) runs the machine in C++
+    ``native`` (default) runs the machine in C++
     (``csrc/wire.cpp``, without the GIL) -- the same opcodes, globals and
     checks as the Python machine below, which the tests hold it to; it
     returns the same RawTensor / RawStorage views."""
 
     def __init__(self, data, native: bool | None = None):
         self.mv = memoryview(data).cast("B")
-        self.native = (_wire is not None) if native is None else native
-        if self.native and _wire is None:
-            raise ImportError("p2pdl_amd._wire is not built (make -C p2pdl_amd/csrc)")
+        self.native = True if native is None else native
 
     def parse(self) -> dict:
         if self.native:
@@ -623,16 +635,54 @@ class PinnedMessage:
 
 def _detached(v):
     """A restricted-machine value with every byte string (a memoryview of
-    the receive buffer) copied out as bytes, at any depth."""
+    the receive buffer) copied out as bytes and every tensor view
+    materialised as a torch tensor on its storage's location (what
+    ``pickle.loads`` gives), at any depth."""
     if isinstance(v, memoryview):
         return bytes(v)
+    if isinstance(v, RawTensor):
+        return v.tensor()
     if isinstance(v, list):
         return [_detached(x) for x in v]
     if isinstance(v, tuple):
         return tuple(_detached(x) for x in v)
     if isinstance(v, dict):
-        return {_detached(a): _detached(b) for a, b in dict.items(v)}
+        d = OrderedDict() if isinstance(v, OrderedDict) else {}
+        for a, b in dict.items(v):
+            d[_detached(a)] = _detached(b)
+        return d
     return v
+
+
+def _envelope_global(module, name):
+    """Globals an envelope may name: only those of a pickled state_dict of
+    tensors (the 'global_model_update' model, aggregation.py:70), each
+    resolved to the restricted machine's own callable (the legacy storage
+    blob is parsed by parse_legacy_storage, never by torch.load)."""
+    fn = _UPDATE_GLOBALS.get((module, name))
+    if fn is None:
+        raise pickle.UnpicklingError(f"refusing to load global {module}.{name} from a peer message")
+    return fn
+
+
+def decode_envelope(mv: memoryview):
+    """A peer's message envelope (node/node.py:112) on the restricted
+    machine: (object, plain) where plain is the decoded dict with byte
+    strings still memoryviews of ``mv`` and tensors still RawTensor views.
+    Every message the reference sends -- 'connect', 'model_update', 'echo',
+    'ready', 'sup' (str / int / bytes / None / lists and dicts of them) and
+    'global_model_update' (a state_dict of tensors) -- decodes here; anything
+    else, or any malformed byte, raises ``pickle.UnpicklingError``.  No
+    stdlib unpickler ever runs on peer bytes."""
+    try:
+        obj, pos = _run_pickle(mv, 0, min_proto=2, resolve_global=_envelope_global)
+    except pickle.UnpicklingError:
+        raise
+    except _MALFORMED as e:
+        raise pickle.UnpicklingError(f"malformed peer message: {type(e).__name__}: {e}") from e
+    if not isinstance(obj, dict) or pos != len(mv):
+        raise pickle.UnpicklingError("a peer message must be one pickled dict")
+    return obj
 
 
 def _dense(rt: "RawTensor") -> bool:
@@ -868,6 +918,27 @@ class DeviceInbox:
             return None
         return m
 
+    @contextlib.contextmanager
+    def consuming(self, stream=None):
+        """The block in which a caller enqueues a kernel that reads slab rows
+        on ``stream`` (default: the current stream of the slab's device),
+        under the landing lock: the stream waits for every row copy ``land``
+        has issued (``order_after_landing``) and is registered as a consumer
+        (``slab_consumed``) BEFORE the kernel is queued, and no ``land`` on
+        another thread runs in between -- one that ran before is covered by
+        the wait, one that runs after records its own wait on this stream
+        after the kernel (registering only after the launch let
+        a land in that window overwrite rows the kernel was reading)."""
+        stream = stream or torch.cuda.current_stream(self.device)
+        raw = stream.cuda_stream
+        with self._lock:
+            for ev in self._events:
+                if ev is not None:
+                    stream.wait_event(ev)
+            if raw not in self._consumers:
+                self._consumers[raw] = (stream, torch.cuda.Event())
+            yield
+
     def slab_consumed(self, stream=None) -> None:
         """Record that a kernel just issued on ``stream`` (default: the current
         stream of the slab's device) reads slab rows: every later ``land``
@@ -934,7 +1005,7 @@ class DeviceInbox:
                     raise RuntimeError(f"update key {key}: shape {rt.size} != {shape}")
                 jobs.append((stage[off:off + n], rt))
             else:  # not part of the fp32 slab: a small tensor of its own
-                out[key] = torch.from_numpy(np.array(rt.array())).to(self.device)
+                out[key] = rt.tensor(self.device)
         _copy_all(jobs)
         with torch.cuda.device(self.device):
             self._wait_rows_free(torch.cuda.current_stream())
@@ -959,24 +1030,21 @@ class DeviceInbox:
         the restricted machine (no globals) and 'model' comes back as a
         ``PinnedMessage`` window of the receive buffer, so ``land`` reads the
         update where it arrived; every other bytes value is real ``bytes``.
-        Any other message -- 'global_model_update' carries a state_dict of
+        Every other message -- 'global_model_update' carries a state_dict of
         tensors (aggregation.py:70), 'echo' / 'ready' / 'sup' carry
-        signatures and whole updates as bytes -- is decoded as the reference
-        decodes it, with every value a plain object.  The handle ``msg`` is
-        consumed: its buffer returns to the pool once no window of it is
-        alive (at once when none escapes)."""
+        signatures and whole updates as bytes -- decodes to the values the
+        reference's ``pickle.loads`` gives (plain objects; tensors on their
+        storage's location), on the same restricted machine
+        (``decode_envelope``): no stdlib unpickler runs on a peer's bytes, and
+        a message it does not accept raises ``pickle.UnpicklingError``.  The
+        handle ``msg`` is consumed: its buffer returns to the pool once no
+        window of it is alive (at once when none escapes)."""
         if not isinstance(msg, PinnedMessage):  # pageable (over the pinned cap)
-            return pickle.loads(msg)
+            return _detached(decode_envelope(memoryview(msg).cast("B")))
         try:
-            mv = msg.view()
-            try:
-                obj, pos = _run_pickle(mv, 0, min_proto=2, resolve_global=_no_global)
-                plain = isinstance(obj, dict) and pos == msg.nbytes
-            except (pickle.UnpicklingError, *_MALFORMED):
-                plain = False
-            if not (plain and dict.get(obj, "type") == "model_update" and isinstance(dict.get(obj, "model"),
-                                                                                 memoryview)):
-                return pickle.loads(mv)  # the reference's own decode of the envelope
+            obj = decode_envelope(msg.view())
+            if not (dict.get(obj, "type") == "model_update" and isinstance(dict.get(obj, "model"), memoryview)):
+                return _detached(obj)
             return {k: (msg.window(v) if k == "model" else _detached(v)) for k, v in dict.items(obj)}
         finally:
             msg.release()
@@ -1013,7 +1081,7 @@ class DeviceInbox:
                                                      f"outside the {msg.nbytes}-byte message")
                     segs.append((src, row_ptr + 4 * off, n))
             else:  # not part of the fp32 slab: a small tensor of its own
-                out[key] = torch.from_numpy(np.array(rt.array())).to(self.device)
+                out[key] = rt.tensor(self.device)
         s = k & 1
         with torch.cuda.device(self.device):
             stream = torch.cuda.current_stream()

@@ -160,6 +160,84 @@ def test_fedavg_large_k64_resnet_shape(cuda):
     assert_bits_equal(got[sl], w_ref, what="cfg2 tail")
 
 
+# The LDS-DMA split kernel (fedavg.hip fedavg_split_kernel) takes the whole
+# 8192-float tiles of a flat buffer of >= 2048 such tiles when K >= 16; the
+# VGPR kernel the rest.  These cases cross that boundary: head, middle, the
+# last split tile, the ragged VGPR tail -- checked against the oracle on
+# windows (the PRNG at the windows' coordinates, oracle.synth_at).
+SPLIT_TILE, SPLIT_MIN_TILES = 8192, 2048
+
+
+def split_windows(n):
+    edge = (n // SPLIT_TILE) * SPLIT_TILE
+    spans = [(0, 3 * SPLIT_TILE + 5), (n // 2 - 7000, n // 2 + 9000), (edge - 2 * SPLIT_TILE - 1, edge + 1),
+             (max(edge - 4099, 0), n)]
+    return [(max(a, 0), min(b, n)) for a, b in spans if a < b]
+
+
+def split_case(dev, k, n, seed, pitch_pad=0, offset=0):
+    """K peers as rows of a pitched slab (row r at r * (n + pitch_pad) + offset
+    floats), filled on the device by the PRNG; w likewise."""
+    pitch = n + pitch_pad
+    slab = torch.empty(k * pitch + offset + 64, dtype=torch.float32, device=dev)
+    rows = [slab[offset + r * pitch: offset + r * pitch + n] for r in range(k)]
+    for r, row in enumerate(rows):
+        ops.fill_synthetic_(row, seed, r, 1e-2)
+    w = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.fill_synthetic_(w, seed, 0xFFFFF, 5e-2)
+    return rows, w
+
+
+def split_expect(k, seed, a, b, torch_gpu=False, kk=None):
+    idx = np.arange(a, b)
+    peers = [oracle.synth_at(idx, seed, p, 1e-2) for p in range(kk if kk is not None else k)]
+    return oracle.fedavg(peers, oracle.synth_at(idx, seed, 0xFFFFF, 5e-2), want_out=True, torch_gpu=torch_gpu)
+
+
+@pytest.mark.parametrize("k,extra,rule", [
+    (16, 4099, "fedavg"),                          # smallest split K, ragged tail with a partial float4
+    (64, 0, "fedavg_torch_gpu"),                   # no tail; torch's GPU division form
+    (256, 3 * SPLIT_TILE + 4097 + 3, "fedavg"),    # cfg3's K; multi-tile tail
+])
+def test_fedavg_split_kernel_vs_oracle(cuda, k, extra, rule):
+    n = SPLIT_MIN_TILES * SPLIT_TILE + extra
+    seed = 0x5B17 + k
+    rows, w = split_case(cuda, k, n, seed, pitch_pad=64)
+    out = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate(rows, rule, w=w, out=out)
+    got_w, got_out = host(w), host(out)
+    for a, b in split_windows(n):
+        w_ref, out_ref = split_expect(k, seed, a, b, torch_gpu=rule == "fedavg_torch_gpu")
+        assert_bits_equal(got_out[a:b], out_ref, what=f"mean [{a}, {b})")
+        assert_bits_equal(got_w[a:b], w_ref, what=f"apply [{a}, {b})")
+
+
+def test_fedavg_split_kernel_unaligned_rows_and_mean_only(cuda):
+    """Rows 4-B but not 16-B aligned: the split kernel's element-wise path,
+    same bits; then the mean alone (no w) through the DMA path."""
+    k, n, seed = 16, SPLIT_MIN_TILES * SPLIT_TILE + 5, 0x5B18
+    rows, w = split_case(cuda, k, n, seed, pitch_pad=1, offset=1)
+    ops.fedavg_apply_(w, rows)
+    got = host(w)
+    for a, b in split_windows(n):
+        assert_bits_equal(got[a:b], split_expect(k, seed, a, b)[0], what=f"unaligned [{a}, {b})")
+    rows, _ = split_case(cuda, k, n, seed, pitch_pad=64)
+    got = host(ops.mean(rows))
+    for a, b in split_windows(n):
+        assert_bits_equal(got[a:b], split_expect(k, seed, a, b)[1], what=f"mean only [{a}, {b})")
+
+
+def test_fedavg_split_kernel_devk(cuda):
+    """The fused cfg5 path: K from device memory (k_max 64, 40 accepted)."""
+    k_max, k, n, seed = 64, 40, SPLIT_MIN_TILES * SPLIT_TILE + 300, 0x5B19
+    rows, w = split_case(cuda, k_max, n, seed, pitch_pad=64)
+    table = ops.pointer_table(rows, cuda)
+    ops.fedavg_apply_devk_(w, table, torch.tensor([k], dtype=torch.int32, device=cuda), k_max)
+    got = host(w)
+    for a, b in split_windows(n):
+        assert_bits_equal(got[a:b], split_expect(k, seed, a, b)[0], what=f"devk [{a}, {b})")
+
+
 def resnet18_param_shapes():
     """The 62 parameter tensors of torchvision's ResNet-18 (11,689,512
     params, BASELINE cfg2), in state_dict order."""

@@ -298,6 +298,36 @@ def test_huge_memo_index_is_cheap():
     assert time.perf_counter() - t0 < 1.0
 
 
+@pytest.mark.parametrize("length", [2 ** 63 - 1, 2 ** 63 - 9, 2 ** 63 - 4096, 2 ** 64 - 1, 2 ** 62])
+def test_binbytes8_huge_length_is_refused(length):
+    """a BINBYTES8 length near INT64_MAX overflowed the
+    C++ machine's bounds check (p + k wrapped negative) and sent the parser
+    past the message.  Both machines must refuse it as a truncated pickle."""
+    body = b"\x80\x05\x95\x00\x00\x00\x00\x00\x00\x00\x00}\x94\x8c\x01a\x94\x8e" + length.to_bytes(8, "little")
+    for data in (body + b"xyz.", body):
+        for parse in PARSERS:
+            with pytest.raises(pickle.UnpicklingError):
+                parse(data)
+
+
+@pytest.mark.parametrize("parse", PARSERS, ids=["python", "native"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_parser_16bit_storages(parse, dtype):
+    """BFloat16Storage payloads parse (held as uint16 bit
+    patterns) and materialise as the torch dtype, bit-equal to pickle.loads."""
+    g = torch.Generator().manual_seed(3)
+    sd = collections.OrderedDict(w=torch.randn(33, 7, generator=g).to(dtype), b=torch.randn(5, generator=g).to(dtype))
+    sd["t"] = sd["w"].t()  # a strided view of the same storage
+    data = pickle.dumps(sd)
+    raw = parse(data)
+    ref = pickle.loads(data)
+    assert list(raw) == list(ref)
+    for key in ref:
+        got = raw[key].tensor("cpu")
+        assert got.dtype == dtype and got.shape == ref[key].shape, key
+        assert torch.equal(got.view(torch.int16), ref[key].contiguous().view(torch.int16)), key
+
+
 def test_recv_message_framing_and_early_close():
     a, b = socket.socketpair()
     msg = pickle.dumps({"type": "model_update", "model": pickle.dumps(mlp_update(2)), "addr": "x", "port": 1})

@@ -115,6 +115,43 @@ def test_other_envelopes_decode_like_the_reference(pageable, kind):
     assert len(pageable.back) == 1
 
 
+class _Boom:
+    def __reduce__(self):
+        return (eval, ("__import__('os').environ.__setitem__('P2P_PWNED', '1')",))
+
+
+@pytest.mark.parametrize("env", [
+    {"type": "model_update", "model": _Boom(), "addr": "a", "port": 1},       # forged GLOBAL / REDUCE
+    {"type": "global_model_update", "model": {"w": _Boom()}, "addr": "a", "port": 1},
+    {"type": "echo", "signature": b"s", "addr": "a", "port": 1, "serialized_state": _Boom()},
+    {"type": "ready", "extra": [1, 2.5]},                                       # an opcode the machine refuses
+])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_no_envelope_reaches_an_unrestricted_unpickler(pageable, env, pinned, monkeypatch):
+    """a message the restricted machine refuses raises
+    UnpicklingError -- it is never handed to pickle.loads (which would run
+    the peer's callable)."""
+    monkeypatch.delenv("P2P_PWNED", raising=False)
+    data = pickle.dumps(env)
+    msg = message(pageable, data) if pinned else bytearray(data)
+    with pytest.raises(pickle.UnpicklingError):
+        open_envelope(msg)
+    import os
+    assert "P2P_PWNED" not in os.environ
+    assert len(pageable.back) == (1 if pinned else 0)  # the buffer went back to the pool
+
+
+def test_global_model_update_16bit_tensors_decode(pageable):
+    """A float16 / bfloat16 global model decodes to the tensors pickle.loads
+    gives (bit-equal, same dtype)."""
+    sd = collections.OrderedDict(a=torch.arange(6.0).to(torch.bfloat16), b=torch.linspace(-2, 2, 9).half())
+    data = pickle.dumps({"type": "global_model_update", "model": sd, "addr": "a", "port": 1})
+    got = open_envelope(message(pageable, data))["model"]
+    assert isinstance(got, collections.OrderedDict) and list(got) == ["a", "b"]
+    for k in sd:
+        assert got[k].dtype == sd[k].dtype and torch.equal(got[k], sd[k]), k
+
+
 def test_pool_is_bounded_by_bytes():
     pool = DeviceInbox.__new__(DeviceInbox)  # the pool's state only
     pool._lock, pool._pinned_free, pool.pool_bytes = threading.Lock(), [], 1000
