@@ -184,27 +184,28 @@ __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const*
 // global_load_lds_dwordx4 nt (1 KiB per wave instruction, no VGPR
 // destination); one barrier per stage: before barrier i each loader waits
 // (vmcnt) for its part of stage i, after it refills the slot stage i-1 used
-// with stage i + kSS - 1, so 2-3 stages (64-96 KiB) are in flight per CU at
-// every moment -- more than one wave can hold (vmcnt is 6 bits: 63 KiB).
+// with stage i + kSS - 1, so 1-2 stages (32-64 KiB) are in flight per CU at
+// every moment beside the one the consumers read.
 // Consumer wave c owns floats [c * kSTile / kSC, (c + 1) * kSTile / kSC) of
 // the tile: ds_read_b128 of its part of stage i and the add, in peer order
 // from +0 (:15, :25-28); after the tile's last peer / K and the apply
 // (:31-38) exactly as fedavg_tile_vec -- the same per-coordinate op order,
-// so the bits are those of the VGPR kernel.  Measured against the VGPR
+// so the bits are those of the VGPR kernel.  128 KiB of LDS per block (3
+// stages + w) leaves a third of the CU's LDS to a kernel running beside it
+// (RCCL's all-gather at N > 1).  Measured against the VGPR
 // kernel, interleaved on one box: cfg3 tile (256 x 125M) +2-3%, 256 x 16M
 // +2-7% across three boxes; the loaders alone (no consumers) reach 6.4-7.0
 // TB/s with this access pattern.
 constexpr int kSL = 4;                       // loader waves
 constexpr int kSC = 8;                       // consumer waves
-constexpr int kSS = 4;                       // ring stages
+constexpr int kSS = 3;                       // ring stages (+ w: 128 KiB of LDS)
 constexpr int kSTile = 8192;                 // floats per tile (32 KiB per peer)
 constexpr int kSPer = kSTile / 256 / kSL;    // DMA instructions per loader per stage
 constexpr int kSRpw = kSTile / 256 / kSC;    // ds_read_b128 per consumer lane per stage
 static_assert((kSS - 2) * kSPer <= 63, "vmcnt is 6 bits");
 static_assert(kSRpw == 4, "lds_read4");
-constexpr int64_t kSGridCap = 2048;          // 8 blocks per CU of 256 (one resident at a time)
+constexpr int kSRoundsPerBlockMax = 8;       // grid <= 8 blocks per CU (one resident at a time)
 constexpr int kSplitMinK = 16;
-constexpr int64_t kSplitMinTiles = 2048;     // below: the tail of too few tiles per CU
 
 #define P2P_LDS __attribute__((address_space(3)))
 template <int AUX>
@@ -324,23 +325,45 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* ag
 
 static int grid_for_tiles(int64_t ntiles) { return static_cast<int>(ntiles > 0 ? ntiles : 1); }
 
-// Flat launches: the split kernel over the whole kSTile tiles of a large
-// buffer (K >= kSplitMinK, >= kSplitMinTiles tiles), the VGPR kernel over
-// the rest (the tail, or all of a smaller buffer).  K is the kernarg or, for
-// the device-K path, k_max.
+// Compute units of the current device (cached per device id).
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cus[dev] = c;
+  }
+  return cus[dev];
+}
+
+// Flat launches.  With K >= kSplitMinK the split kernel takes whole ROUNDS of
+// kSTile tiles -- a multiple of the CU count, one block resident per CU, so
+// every CU gets the same number of 32-KiB x K tiles -- and the VGPR kernel
+// the rest (fewer than one tile per CU, plus the ragged tail), in 4096-float
+// tiles that many blocks share per CU: 1907 tiles (a cfg3 chunk at 8 GPUs) as
+// 8 split rounds would leave half the CUs idle in the last one.  The grid is
+// CUs x R blocks with R the largest divisor of the round count <= 8 (equal
+// tiles per block).  K is the kernarg or, for the device-K path, k_max.
 static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,
                         float lr, hipStream_t stream, bool recip = false) {
-  const int64_t full = K >= kSplitMinK ? n / kSTile : 0;
   int64_t done = 0;
-  if (full >= kSplitMinTiles) {
-    const dim3 grid(static_cast<unsigned>(full < kSGridCap ? full : kSGridCap));
-    const dim3 block(64 * (kSL + kSC));
-    if (recip)
-      hipLaunchKernelGGL(fedavg_split_kernel<true>, grid, block, 0, stream, peers, K, k_dev, full, w, out, lr);
-    else
-      hipLaunchKernelGGL(fedavg_split_kernel<false>, grid, block, 0, stream, peers, K, k_dev, full, w, out, lr);
-    done = full * kSTile;
-    if (done == n) return;
+  if (K >= kSplitMinK) {
+    const int64_t cus = device_cus();
+    const int64_t rounds = n / kSTile / cus;
+    if (rounds >= 1) {
+      int64_t r = kSRoundsPerBlockMax < rounds ? kSRoundsPerBlockMax : rounds;
+      while (rounds % r) --r;
+      const int64_t tiles = rounds * cus;
+      const dim3 grid(static_cast<unsigned>(cus * r)), block(64 * (kSL + kSC));
+      if (recip)
+        hipLaunchKernelGGL(fedavg_split_kernel<true>, grid, block, 0, stream, peers, K, k_dev, tiles, w, out, lr);
+      else
+        hipLaunchKernelGGL(fedavg_split_kernel<false>, grid, block, 0, stream, peers, K, k_dev, tiles, w, out, lr);
+      done = tiles * kSTile;
+      if (done == n) return;
+    }
   }
   static_assert(kSTile % kTile == 0, "split tiles are whole VGPR tiles");
   const int64_t tile_base = done / kTile;

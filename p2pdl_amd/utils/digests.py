@@ -177,6 +177,18 @@ _POOL_PREFIX = "p2p-sha256"
 _POOL_LOCK = threading.Lock()
 
 
+def hash_threads() -> int:
+    """Hashing threads: this process's CPU affinity, capped by
+    OMP_NUM_THREADS when the environment sets it (the GPU box exports 16, one
+    GPU's share of its host cores; os.cpu_count() there counts the whole
+    machine).  bench.py's hashlib baseline uses the same rule
+    (oracle/cpu_baseline.py host_threads), so the two rates compare like for
+    like."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return min(aff, int(env)) if env.isdigit() and int(env) > 0 else aff
+
+
 def hash_pool():
     """Host hashing threads (hashlib releases the GIL on large buffers)."""
     global _POOL
@@ -184,7 +196,7 @@ def hash_pool():
         if _POOL is None:
             from concurrent.futures import ThreadPoolExecutor
 
-            _POOL = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1), thread_name_prefix=_POOL_PREFIX)
+            _POOL = ThreadPoolExecutor(max_workers=hash_threads(), thread_name_prefix=_POOL_PREFIX)
         return _POOL
 
 

@@ -95,3 +95,56 @@ def test_fused_path_wrappers_check_shapes_before_the_launch():
         ops.fedavg_apply_devk_(w, tbl, cnt.long(), 3)
     with pytest.raises(ValueError, match="out has"):
         ops.fedavg_apply_devk_(w, tbl, cnt, 3, out=torch.zeros(9))
+
+
+@pytest.mark.gpu
+def test_cfg5_product_route_at_k256(cuda):
+    """cfg5 at its configuration's K (VERDICT r04 next #3a): 256 device-
+    resident serialized updates of >= 2 staging pieces each, ~10% corrupted,
+    through the product route bench.py's cfg5 times --
+    digest_device_messages (host SHA threads, pipelined D2H) -> digest_accept
+    -> fedavg_apply_devk_ (K from the device, k_max = 256) -- against
+    hashlib (what the senders signed, node/node.py:285 -> utils/crypto.py:56)
+    and the FedAvg oracle over the accepted updates in list order
+    (aggregation.py:15-38)."""
+    import oracle  # checker only
+    from p2pdl_amd import ops
+
+    K, hdr = 256, 64
+    n = (2 * dg.STAGE + 12345) // 4  # fp32 payload: each message spans 3 staging pieces
+    msg = hdr + 4 * n
+    stride = -(-msg // 256) * 256
+    seed = 0x5EED0C05
+    buf = torch.zeros(K * stride, dtype=torch.uint8, device=cuda)
+    offsets = [p * stride for p in range(K)]
+    for p in range(K):
+        buf[offsets[p]:offsets[p] + hdr] = torch.tensor(list((b"update %05d " % p).ljust(hdr, b"\0")),
+                                                       dtype=torch.uint8, device=cuda)
+        ops.fill_synthetic_(buf[offsets[p] + hdr:offsets[p] + msg].view(torch.float32), seed, p, 1e-2)
+    host = buf.cpu().numpy()
+    signed = [hashlib.sha256(host[o:o + msg].tobytes()).digest() for o in offsets]
+    expected = torch.tensor(np.frombuffer(b"".join(signed), dtype=np.uint8).reshape(K, 32), device=cuda)
+    bad = [p for p in range(K) if (p * 7919) % 10 == 3]
+    for p in bad:  # corrupted in flight: one payload byte
+        buf[offsets[p] + hdr + 1000 + p] ^= 0x40
+    digests = dg.digest_device_messages(buf, offsets, [msg] * K)
+    got = digests.cpu().numpy()
+    for p in range(K):
+        assert (bytes(got[p]) == signed[p]) == (p not in bad), p
+    payload_tbl = torch.tensor([buf.data_ptr() + o + hdr for o in offsets], dtype=torch.int64, device=cuda)
+    accepted = torch.zeros(K, dtype=torch.int64, device=cuda)
+    count = torch.zeros(1, dtype=torch.int32, device=cuda)
+    w = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.fill_synthetic_(w, seed, 0xFFFFF, 5e-2)
+    ops.digest_accept(digests, expected, payload_tbl, accepted, count)
+    ops.fedavg_apply_devk_(w, accepted, count, K)
+    keep = [p for p in range(K) if p not in bad]
+    assert int(count.item()) == len(keep)
+    tbl = payload_tbl.cpu().tolist()
+    assert accepted.cpu().tolist()[:len(keep)] == [tbl[p] for p in keep]  # list order
+    wh = w.cpu().numpy()
+    for a, b in [(0, 5000), (n // 2, n // 2 + 9000), (n - 70_000, n)]:
+        idx = np.arange(a, b)
+        want, _ = oracle.fedavg([oracle.synth_at(idx, seed, p, 1e-2) for p in keep],
+                                oracle.synth_at(idx, seed, 0xFFFFF, 5e-2))
+        assert np.array_equal(wh[a:b].view(np.uint32), want.view(np.uint32)), (a, b)

@@ -160,18 +160,19 @@ def test_fedavg_large_k64_resnet_shape(cuda):
     assert_bits_equal(got[sl], w_ref, what="cfg2 tail")
 
 
-# The LDS-DMA split kernel (fedavg.hip fedavg_split_kernel) takes the whole
-# 8192-float tiles of a flat buffer of >= 2048 such tiles when K >= 16; the
-# VGPR kernel the rest.  These cases cross that boundary: head, middle, the
-# last split tile, the ragged VGPR tail -- checked against the oracle on
-# windows (the PRNG at the windows' coordinates, oracle.synth_at).
+# The LDS-DMA split kernel (fedavg.hip fedavg_split_kernel) takes whole
+# rounds of 8192-float tiles (a multiple of the CU count) of a flat buffer
+# when K >= 16; the VGPR kernel the rest.  These cases cross that boundary:
+# head, middle, the last split tile, the VGPR remainder and ragged tail --
+# checked against the oracle on windows (the PRNG at the windows'
+# coordinates, oracle.synth_at).
 SPLIT_TILE, SPLIT_MIN_TILES = 8192, 2048
 
 
-def split_windows(n):
-    edge = (n // SPLIT_TILE) * SPLIT_TILE
-    spans = [(0, 3 * SPLIT_TILE + 5), (n // 2 - 7000, n // 2 + 9000), (edge - 2 * SPLIT_TILE - 1, edge + 1),
-             (max(edge - 4099, 0), n)]
+def split_windows(n, cus=256):
+    edge = (n // SPLIT_TILE // cus) * cus * SPLIT_TILE  # end of the split rounds
+    spans = [(0, 3 * SPLIT_TILE + 5), (n // 2 - 7000, n // 2 + 9000), (edge - 2 * SPLIT_TILE - 1, edge + 4099),
+             (max(n - 4099, 0), n)]
     return [(max(a, 0), min(b, n)) for a, b in spans if a < b]
 
 
@@ -194,13 +195,12 @@ def split_expect(k, seed, a, b, torch_gpu=False, kk=None):
     return oracle.fedavg(peers, oracle.synth_at(idx, seed, 0xFFFFF, 5e-2), want_out=True, torch_gpu=torch_gpu)
 
 
-@pytest.mark.parametrize("k,extra,rule", [
-    (16, 4099, "fedavg"),                          # smallest split K, ragged tail with a partial float4
-    (64, 0, "fedavg_torch_gpu"),                   # no tail; torch's GPU division form
-    (256, 3 * SPLIT_TILE + 4097 + 3, "fedavg"),    # cfg3's K; multi-tile tail
+@pytest.mark.parametrize("k,n,rule", [
+    (16, SPLIT_MIN_TILES * SPLIT_TILE + 4099, "fedavg"),   # smallest split K, ragged tail with a partial float4
+    (64, SPLIT_MIN_TILES * SPLIT_TILE, "fedavg_torch_gpu"),  # no tail; torch's GPU division form
+    (256, 1907 * SPLIT_TILE + 4097 + 3, "fedavg"),         # cfg3's K and its 8-GPU chunk: 7 rounds + 115 tiles + tail
 ])
-def test_fedavg_split_kernel_vs_oracle(cuda, k, extra, rule):
-    n = SPLIT_MIN_TILES * SPLIT_TILE + extra
+def test_fedavg_split_kernel_vs_oracle(cuda, k, n, rule):
     seed = 0x5B17 + k
     rows, w = split_case(cuda, k, n, seed, pitch_pad=64)
     out = torch.empty(n, dtype=torch.float32, device=cuda)
