@@ -169,6 +169,18 @@ def roofline(alg_bytes: float, kern_ms: float, traffic, **extra) -> dict:
                  "alg_bytes_per_launch": int(alg_bytes)}, **extra)
 
 
+def dist_info() -> dict:
+    """What ran the exchange: the process group's world size and backend,
+    and the RCCL version torch was built against."""
+    info = {"world_size": dist.get_world_size(), "backend": dist.get_backend()}
+    try:
+        v = torch.cuda.nccl.version()
+        info["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception as e:  # noqa: BLE001 -- a record field, never fatal
+        info["rccl_version"] = f"unknown ({type(e).__name__})"
+    return info
+
+
 def parallelism(c: Ctx) -> str:
     if c.world == 1:
         return "single GPU"
@@ -189,6 +201,24 @@ def oracle_expect(rule, K, m, seed, chunk=0, nranks=1, rank=0):
     else:
         want, _ = oracle.robust(peers, rid, ops.trim_count(K) if rid == 2 else 0, w=w0)
     return want
+
+
+def kernel_only_ms(fn, reps: int, stream=None) -> float:
+    """Mean GPU time of the work ``fn`` enqueues, alone: the stream is kept
+    busy by a spin kernel while the start event, the launch and the end event
+    are queued behind it, so the host's launch overhead never shows between
+    the events (for a ~5 us kernel it otherwise dominates)."""
+    stream = stream or torch.cuda.current_stream()
+    ev = []
+    for _ in range(reps):
+        torch.cuda._sleep(3_000_000)  # ~1.5 ms of spinning: the launch below is queued behind it
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / len(ev)
 
 
 def bits_equal(a, b) -> bool:
@@ -233,6 +263,8 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
     comm = torch.cuda.Stream(dev)
     kern = []
 
+    gath = []
+
     def step(record=False):
         for s in range(S):
             ws = w[s, :C]
@@ -248,7 +280,13 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
                 done.record(comp)
                 comm.wait_event(done)
                 with torch.cuda.stream(comm):
+                    if record:
+                        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        g0.record(comm)
                     dist.all_gather_into_tensor(w_full[s * C * world:(s + 1) * C * world], ws)
+                    if record:
+                        g1.record(comm)
+                        gath.append((g0, g1))
         if world > 1:
             comp.wait_stream(comm)
 
@@ -285,6 +323,16 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = sum(a.elapsed_time(b) for a, b in kern) / len(kern)
+    per_rank = None
+    if world > 1:
+        # every rank's kernel and all-gather sums per step (the diagnosis of a
+        # slow or stuck rank: which side of the pipeline it lost time on)
+        mine = torch.tensor([rank, sum(a.elapsed_time(b) for a, b in kern) / steps,
+                             sum(a.elapsed_time(b) for a, b in gath) / steps], dtype=torch.float64, device=dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [{"rank": int(t[0]), "kernel_ms_per_step": round(float(t[1]), 3),
+                     "allgather_ms_per_step": round(float(t[2]), 3)} for t in (x.cpu() for x in allr)]
     ref_s = None
     if rule == "fedavg" and world == 1 and not args.no_reference_gpu:
         # the reference's aggregation loop (aggregator/aggregation.py:15-38) as a
@@ -335,6 +383,7 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
                    "rule": rule, "peers": K, "coords_per_gpu": n, "coords_total": n * world,
                    "parallelism": parallelism(c),
                    "pct_hbm_peak_step": round(4 * n * (K + 2) / step_s / 1e9 / HBM_PEAK_GBS, 4)}
+                  | ({"per_rank": per_rank, "chunks_per_rank": S, "chunk_coords": C} | dist_info() if per_rank else {})
                   | ({"reference_on_gpu_ms_per_step": round(ref_s * 1e3, 3),
                       "speedup_vs_reference_on_gpu": round(ref_s / step_s, 2)} if ref_s else {}),
         "roofline": roofline(4 * C * (K + 2), kern_ms, traffic_for(name, C, K)),
@@ -420,10 +469,15 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
         gath.append(g_tot)
     best = min(range(passes), key=lambda i: wall[i])  # best pass (each pass is the whole job)
     tot, k_ms, g_ms = wall[best], kern[best], gath[best]
+    per_rank = None
     if world > 1:
-        t = torch.tensor([tot, k_ms, g_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        tot, k_ms, g_ms = (float(x) for x in t.tolist())
+        mine = torch.tensor([rank, tot, k_ms, g_ms], dtype=torch.float64, device=dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        rows = [x.cpu().tolist() for x in allr]
+        per_rank = [{"rank": int(r[0]), "ms_per_job": round(r[1], 3), "kernel_ms_sum": round(r[2], 3),
+                     "allgather_ms_sum": round(r[3], 3)} for r in rows]
+        tot, k_ms, g_ms = (max(r[i] for r in rows) for i in (1, 2, 3))
     del slab, w, w_full, tables
     torch.cuda.empty_cache()
     peer_bytes = K * CFG3_COORDS * 4
@@ -433,7 +487,8 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
         "scaling": "strong", "dtype": "fp32",
         "config": {"workload": f"cfg3 full job: fedavg over {K} peers x {CFG3_COORDS:,} fp32 coords "
                                f"({peer_bytes/1e12:.3f} TB); {per} tile(s) of {T:,} coords per GPU, "
-                               f"{chunks} chunks per tile", "tiles_per_gpu": per, "parallelism": parallelism(c),
+                               f"{chunks} chunks per tile", "tiles_per_gpu": per, "parallelism": parallelism(c)}
+                  | ({"per_rank": per_rank} | dist_info() if per_rank else {}) | {
                    "timing": "sum over tiles of first-kernel-start -> last-all-gather-end (HIP events; "
                              "all-gather of chunk s overlapped with chunk s+1); inputs regenerated per tile "
                              "outside the timed region (1.02 TB > 288 GB HBM)"},
@@ -584,6 +639,16 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
             call(record=True)
         torch.cuda.synchronize()
         ev_fast = list(ev)
+        # the segment kernel alone: the launch aggregate_models cached on the
+        # validated model-state entry (ops.relaunch: no table work), queued
+        # behind a spin so no host time falls between the events
+        from p2pdl_amd.aggregator.model_state import model_state
+
+        _, ws_m, st_m = model_state(model)
+        launch = st_m.extra.get("launch") if st_m is not None else None
+        kernel_ms = None
+        if launch is not None:
+            kernel_ms = kernel_only_ms(lambda: ops.relaunch(launch[2], dev, len(ws_m), K, 0.1), steps, comp)
         # the general path (plain dicts of tensors, e.g. from pickle.loads):
         # the peer table gathered in C from the L x K update tensors
         updates = plain
@@ -635,11 +700,14 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
                    "us_per_call": round(step_s * 1e6, 1), "us_per_call_general_path": round(general_s * 1e6, 1)}
                   | ({"reference_on_gpu_us_per_call": round(ref_s * 1e6, 1),
                       "speedup_vs_reference_on_gpu": round(ref_s / step_s, 1)} if ref_s else {}),
-        "roofline": roofline(4 * n * (K + 2), call_ms, traffic_for(name, n, K),
-                             timing="HIP events around aggregate_models (table H2D + segment kernel), in a "
-                                    "pass after the timed loops (value / us_per_call: host wall time, no events)",
+        "roofline": roofline(4 * n * (K + 2), kernel_ms or call_ms, traffic_for(name, n, K),
+                             timing=("the segment kernel alone: HIP events around the cached launch "
+                                     "(ops.relaunch) queued behind a spin kernel; call_ms: events around the "
+                                     "whole aggregate_models call; value / us_per_call: host wall time, no events"
+                                     if kernel_ms else "HIP events around aggregate_models (no cached launch)"),
+                             call_ms=round(call_ms, 4),
                              flat_kernel_ms=round(flat_ms, 4),
-                             vs_flat_kernel=round(flat_ms / call_ms, 4)),
+                             vs_flat_kernel=round(flat_ms / (kernel_ms or call_ms), 4)),
         "cpu_baseline": cpu,
     }
 
@@ -1341,8 +1409,9 @@ def replica_workload(args, name, dev):
 
 # ------------------------------------------------------------------ main
 SUB_KEEP = ("us_per_call", "us_per_call_general_path", "ms_per_job", "kernel_ms_sum", "allgather_ms_sum")
-ROOF_KEEP = ("kernel_ms", "vs_flat_kernel", "fedavg_ms", "chain_issue_bound_gbs", "digest_route", "gpu_kernel_gbs",
-             "frac_of_host_sha_bound")
+ROOF_KEEP = ("bound", "kernel_ms", "call_ms", "vs_flat_kernel", "digest_route", "digest_ms", "host_sha_bound_gbs",
+             "pcie_d2h_gbs", "fedavg_kernel_ms", "fedavg_frac_of_hbm_peak", "sha256_kernel_gbs")
+CFG_KEEP = ("per_rank", "world_size", "rccl_version")
 
 
 def compact_sub(rec: dict) -> dict:
@@ -1363,6 +1432,7 @@ def compact_sub(rec: dict) -> dict:
         if alg and tr:
             out["traffic_x"] = round(tr / alg, 5)
     cfg = rec.get("config") or {}
+    out.update({k: cfg[k] for k in CFG_KEEP if k in cfg})
     for k in ("reference_ms", "staging_ms", "pinned_digest_overlapped_ms", "with_digest", "hashes_product",
               "speedup_vs_reference", "joined_ms", "reference_on_gpu_ms_per_step", "speedup_vs_reference_on_gpu"):
         if k in cfg:
@@ -1373,6 +1443,37 @@ def compact_sub(rec: dict) -> dict:
         out["cpu"] = {k: cpu[k] for k in ("value", "unit", "cores", "value_1thread", "us_per_call", "kind")
                       if k in cpu}
     return out
+
+
+HBM_BYTES = 288e9
+XGMI_LINK_GBS = 153.0  # one xGMI link (7 per GPU): a single ring's per-link bound
+
+
+def scale_plan(world: int, n1: dict, *, steps: int = 10, warmup: int = 2, chunks: int = 8,
+               fill_tbs: float = 1.0, startup_s: float = 120.0) -> dict:
+    """The default line's footprint and run time at ``world`` GPUs, predicted
+    from the measured N = 1 line ``n1`` (its ms_per_step and sub.cfg3_full
+    ms_per_job) -- no GPU needed.  Per rank: the main line's resident [K, n]
+    slab + w + the all-gathered model, then cfg3_full's 125M-coordinate tile
+    + the 1B-coordinate model; time: the inputs generated on device (at
+    ``fill_tbs``), warmup + timed steps, cfg3_full's 8 / world tiles per pass
+    (two passes), each chunk's all-gather bounded by one ring per link, and a
+    fixed allowance for the first torch import and RCCL's setup."""
+    K, n = 256, CFG3_TILE
+    main_bytes = (K + 2 + world) * n * 4 if world > 1 else (K + 2) * n * 4
+    full_bytes = K * CFG3_TILE * 4 + CFG3_TILE * 4 + (CFG3_COORDS * 4 if world > 1 else 0)
+    step_ms = float(n1["ms_per_step"])
+    C = n // chunks
+    gather_ms = 0.0 if world == 1 else chunks * C * 4 * (world - 1) / (XGMI_LINK_GBS * 1e9) * 1e3
+    step_pred = max(step_ms, gather_ms) + (gather_ms / chunks if world > 1 else 0.0)  # the last chunk's gather
+    tiles = CFG3_COORDS // CFG3_TILE // world
+    job_ms = float(n1["sub"]["cfg3_full"]["ms_per_job"]) * tiles / (CFG3_COORDS // CFG3_TILE) if n1.get("sub") else \
+        step_ms * tiles
+    fill_s = (K + 1) * n * 4 / (fill_tbs * 1e12)
+    total_s = startup_s + fill_s + (steps + warmup) * step_pred / 1e3 + 2 * tiles * (fill_s + job_ms / 1e3)
+    return {"world": world, "bytes_per_rank": max(main_bytes, full_bytes), "fits_hbm": max(main_bytes, full_bytes)
+            < 0.97 * HBM_BYTES, "step_ms": round(step_pred, 3), "allgather_ms_per_step": round(gather_ms, 3),
+            "seconds": round(total_s, 1)}
 
 
 def launch_plan(gpus: int, env, visible: int, backend: str):
@@ -1433,12 +1534,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % max(1, visible)
     if world > 1:
+        import datetime
+
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
+        # a collective stuck longer than this ends the rank non-zero with the
+        # collective named (the process group's watchdog), well inside the
+        # driver's run limit, instead of a silent hang
+        tmo = datetime.timedelta(seconds=float(os.environ.get("P2P_DIST_TIMEOUT_S", "240")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
         if dist.get_world_size() != world:
             raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, expected {world}")
     dev = torch.device("cuda", local)

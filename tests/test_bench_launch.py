@@ -57,3 +57,39 @@ def test_mismatch_exits_nonzero_before_any_gpu_work(tmp_path):
                        text=True, timeout=300)
     assert p.returncode != 0
     assert "WORLD_SIZE=2" in p.stderr and not p.stdout.strip()
+
+
+def _n1_line():
+    """The newest committed N = 1 default line with the cfg3_full sub-record."""
+    import glob
+    import json
+
+    for path in sorted(glob.glob(os.path.join(os.path.dirname(bench.__file__), "profiles", "r0*", "**", "*.json"),
+                                 recursive=True), reverse=True):
+        try:
+            with open(path) as f:
+                rec = json.loads(f.readline())
+        except (ValueError, OSError):
+            continue
+        if isinstance(rec, dict) and rec.get("n_gpus") == 1 and "cfg3_full" in (rec.get("sub") or {}):
+            return rec
+    return {"ms_per_step": 21.0, "sub": {"cfg3_full": {"ms_per_job": 170.0}}}  # round 4's measured line
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_scale_plan_fits_hbm_and_the_driver_limit(world):
+    """the driver's first N = 8 run must fit one
+    MI355X's 288 GB per rank and its 600 s, by the N = 1 measurements."""
+    plan = bench.scale_plan(world, _n1_line())
+    assert plan["fits_hbm"], plan
+    assert plan["seconds"] < 600, plan
+    if world == 8:  # the all-gather of a step (3.5 GB received per rank) stays below the reduction
+        assert plan["allgather_ms_per_step"] < 2 * plan["step_ms"], plan
+
+
+def test_init_process_group_has_a_timeout():
+    """A stuck RCCL collective ends the rank (the process group watchdog)
+    instead of hanging the driver's run: bench.py passes timeout=."""
+    src = open(bench.__file__).read()
+    assert 'init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)' in src
+    assert "init_process_group(backend, timeout=tmo)" in src
