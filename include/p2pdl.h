@@ -36,8 +36,10 @@ extern "C" {
  *    gone; every other entry point is unchanged.
  * 3: adds p2p_land_segments_f32 (K5, landing a received update).
  * 4: adds the rule P2P_RULE_FEDAVG_TORCH_GPU and p2p_fedavg_apply_16
- *    (float16 / bfloat16 models). */
-#define P2P_ABI_VERSION 4
+ *    (float16 / bfloat16 models).
+ * 5: P2P_DELTA_TILE 4096 -> 1024 (the delta segment table's tile_begin is
+ *    counted in 1024-element tiles). */
+#define P2P_ABI_VERSION 5
 
 typedef void *p2p_stream_t; /* hipStream_t */
 
@@ -138,7 +140,7 @@ int32_t p2p_apply_f32(float *w, const float *agg, float lr, int64_t n, p2p_strea
 int32_t p2p_delta_snapshot_f32(const float *cur, float *prev, float *delta, int64_t n, int32_t first,
                                p2p_stream_t stream);
 
-#define P2P_DELTA_TILE 4096 /* elements per tile of the delta segment kernel */
+#define P2P_DELTA_TILE 1024 /* elements per tile of the delta segment kernel */
 
 /* One tensor of a state_dict for the delta kernel (device-resident entry). */
 typedef struct p2p_delta_segment_t {

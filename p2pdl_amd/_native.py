@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # P2P_LIB selects a diagnostic build (csrc/Makefile `diag`); default: the product library
 LIB_PATH = os.environ.get("P2P_LIB") or os.path.join(_HERE, "libp2pdl_hip.so")
-ABI_VERSION = 4  # include/p2pdl.h P2P_ABI_VERSION
+ABI_VERSION = 5  # include/p2pdl.h P2P_ABI_VERSION
 
 P2P_RULE_FEDAVG, P2P_RULE_MEDIAN, P2P_RULE_TRIMMED, P2P_RULE_FEDAVG_TORCH_GPU = 0, 1, 2, 3
 P2P_DTYPE_F16, P2P_DTYPE_BF16 = 1, 2

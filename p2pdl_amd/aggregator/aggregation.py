@@ -303,10 +303,17 @@ def _consuming(received):
         u = rm.get("model") if isinstance(rm, dict) else None
         if isinstance(u, LandedUpdate):
             inboxes[id(u.inbox)] = u.inbox
+    if not inboxes:
+        return _NO_INBOX
+    if len(inboxes) == 1:
+        return next(iter(inboxes.values())).consuming()
     stack = contextlib.ExitStack()
     for inbox in inboxes.values():
         stack.enter_context(inbox.consuming())
     return stack
+
+
+_NO_INBOX = contextlib.nullcontext()
 
 
 def broadcast_global_model_update(self):

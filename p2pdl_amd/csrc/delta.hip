@@ -10,16 +10,21 @@
 // coordinate, HBM-bound (0.0625 flop/B).  fp32 subtraction is IEEE, so the
 // result is bit-exact with torch's CPU/GPU `-`.
 //
-// Layout as K1 (fedavg.hip): a 256-lane block owns a 4096-float tile, lane l
-// the float4s l, l+256, l+512, l+768 -> every wave instruction moves one
-// contiguous 1 KiB.  Misaligned views and ragged tails go element-wise.
+// Layout: a 256-lane block owns a 1024-float tile, lane l its float4 l ->
+// every wave instruction moves one contiguous 1 KiB.  One float4 per lane
+// (round 5, tools/delta_lab.hip policy mode, profiles/r05/lab4): 0.767-0.773
+// of HBM peak against 0.748-0.758 for four per lane (rounds 1-4), nontemporal
+// loads and stores both (each plain variant is 1.5-4% slower), on a box
+// whose plain float4 copy reads 0.75-0.78.  Misaligned views and ragged
+// tails go element-wise.
 #include "p2p_common.h"
 
 namespace p2p {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
-constexpr int kDNV = 4;
-constexpr int kDTile = kBlock * 4 * kDNV;  // 4096 floats
+constexpr int kDNV = 1;
+constexpr int kDTile = kBlock * 4 * kDNV;  // 1024 floats == P2P_DELTA_TILE
+static_assert(kDTile == P2P_DELTA_TILE, "the ABI's delta tile");
 
 __device__ __forceinline__ f4 ld4_nt(const float* p) { return ldg_nt(reinterpret_cast<const f4*>(p)); }
 __device__ __forceinline__ void st4_nt(float* p, f4 v) {
@@ -112,7 +117,7 @@ extern "C" int32_t p2p_delta_snapshot_f32(const float* cur, float* prev, float* 
       3)
     return P2P_ERR_ALIGN;
   if (n == 0) return P2P_OK;
-  // 4 float4 per lane per tensor with nontemporal stores: the fastest of the
+  // one float4 per lane, nontemporal loads and stores: the fastest of the
   // NV in {1, 2, 4, 8} x {plain, nontemporal} grid measured.
   const int64_t tiles = ceil_div(n, kDTile);
   if (tiles > 0x7FFFFFFFll) return P2P_ERR_UNSUPPORTED;

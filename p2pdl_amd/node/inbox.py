@@ -35,7 +35,6 @@ this on torch-produced pickles of the reference's message shapes).
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import os
 import pickle
@@ -763,6 +762,37 @@ class LandedUpdate(OrderedDict):
 ROW_ALIGN = 64  # fp32 elements (256 B) per tensor offset in a slab row
 
 
+class _Consuming:
+    """DeviceInbox.consuming(): the landing lock held around a launch."""
+
+    __slots__ = ("inbox", "stream")
+
+    def __init__(self, inbox, stream):
+        self.inbox, self.stream = inbox, stream
+
+    def __enter__(self):
+        from .. import _native as N
+
+        ib, stream = self.inbox, self.stream
+        ib._lock.acquire()
+        try:
+            events = [e for e in ib._events if e is not None]
+            raw = stream.cuda_stream if stream is not None else N.stream_handle(ib.device)
+            if events or raw not in ib._consumers:
+                stream = stream or torch.cuda.current_stream(ib.device)
+                for ev in events:
+                    stream.wait_event(ev)
+                ib._consumers.setdefault(raw, (stream, torch.cuda.Event()))
+        except BaseException:
+            ib._lock.release()
+            raise
+        return self
+
+    def __exit__(self, *exc):
+        self.inbox._lock.release()
+        return False
+
+
 class DeviceInbox:
     """[K_max, N] fp32 slab on the GPU for the updates of one round.
 
@@ -918,8 +948,7 @@ class DeviceInbox:
             return None
         return m
 
-    @contextlib.contextmanager
-    def consuming(self, stream=None):
+    def consuming(self, stream=None) -> "_Consuming":
         """The block in which a caller enqueues a kernel that reads slab rows
         on ``stream`` (default: the current stream of the slab's device),
         under the landing lock: the stream waits for every row copy ``land``
@@ -928,16 +957,9 @@ class DeviceInbox:
         another thread runs in between -- one that ran before is covered by
         the wait, one that runs after records its own wait on this stream
         after the kernel (registering only after the launch let
-        a land in that window overwrite rows the kernel was reading)."""
-        stream = stream or torch.cuda.current_stream(self.device)
-        raw = stream.cuda_stream
-        with self._lock:
-            for ev in self._events:
-                if ev is not None:
-                    stream.wait_event(ev)
-            if raw not in self._consumers:
-                self._consumers[raw] = (stream, torch.cuda.Event())
-            yield
+        a land in that window overwrite rows the kernel was reading).  A
+        plain class, not a generator context: cfg1's whole call is ~12 us."""
+        return _Consuming(self, stream)
 
     def slab_consumed(self, stream=None) -> None:
         """Record that a kernel just issued on ``stream`` (default: the current

@@ -437,7 +437,7 @@ def relaunch(entry, dev, L: int, K: int, lr: float) -> None:
 
 
 # ------------------------------------------------------------------ K4
-DELTA_TILE = 4096  # == P2P_DELTA_TILE
+DELTA_TILE = 1024  # == P2P_DELTA_TILE
 _DSEG_DTYPE = np.dtype([("cur", "<u8"), ("prev", "<u8"), ("delta", "<u8"), ("n", "<i8"),
                         ("tile_begin", "<i8")])  # == p2p_delta_segment_t (40 B)
 

@@ -749,7 +749,7 @@ def test_delta_beyond_2g_elements_sampled(cuda):
 
 
 # ------------------------------------------------------------------ K4 trainer delta
-@pytest.mark.parametrize("n", [1, 3, 4096, 4097, 100_003])
+@pytest.mark.parametrize("n", [1, 3, 1023, 1024, 1025, 4096, 4097, 100_003])
 @pytest.mark.parametrize("first", [False, True])
 def test_delta_snapshot_flat(cuda, n, first):
     cur = oracle.synth(n, 21, 1, 1e-1)
@@ -768,7 +768,7 @@ def test_delta_snapshot_flat(cuda, n, first):
 
 
 def test_delta_snapshot_unaligned_and_segments(cuda):
-    sizes = [1, 5, 4095, 4096, 4099, 70_001]
+    sizes = [1, 5, 1023, 1024, 1025, 4095, 4096, 4099, 70_001]
     n = sum(sizes)
     cur = oracle.synth(n + 1, 22, 1, 1e-1)
     prev = oracle.synth(n + 1, 22, 2, 1e-1)

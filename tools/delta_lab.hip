@@ -77,6 +77,49 @@ __global__ __launch_bounds__(256) void chunk_k(const float* cur, float* prev, fl
   }
 }
 
+// Round 5: the cache policy of loads and stores, for a
+// copy and for the delta, same box, same sizes: LNT / SNT = nontemporal
+// loads / stores, else plain (default policy).
+template <bool LNT>
+__device__ __forceinline__ f4 ldp(const float* p) {
+  if constexpr (LNT) return __builtin_nontemporal_load((const G f4*)p);
+  else return *(const G f4*)p;
+}
+template <bool SNT>
+__device__ __forceinline__ void stpol(float* p, f4 v) {
+  if constexpr (SNT) __builtin_nontemporal_store(v, (G f4*)p);
+  else *(G f4*)p = v;
+}
+template <int NV, bool LNT, bool SNT>
+__global__ __launch_bounds__(256) void copy_pol(const float* a, float* b, long n) {
+  const long base = (long)blockIdx.x * (1024 * NV) + 4 * threadIdx.x;
+  f4 c[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) c[v] = ldp<LNT>(a + base + 1024 * v);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) stpol<SNT>(b + base + 1024 * v, c[v]);
+}
+// grid-stride float4 copy, one float4 per lane per trip (a STREAM-style copy)
+template <bool LNT, bool SNT>
+__global__ __launch_bounds__(256) void copy_gs(const float* a, float* b, long n4) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256)
+    stpol<SNT>(b + 4 * i, ldp<LNT>(a + 4 * i));
+}
+template <int NV, bool LNT, bool SNT, int BL>
+__global__ __launch_bounds__(BL) void delta_pol(const float* cur, float* prev, float* delta, long n) {
+  const long base = (long)blockIdx.x * (4 * BL * NV) + 4 * threadIdx.x;
+  f4 c[NV], p[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) c[v] = ldp<LNT>(cur + base + 4 * BL * v);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) p[v] = ldp<LNT>(prev + base + 4 * BL * v);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    stpol<SNT>(delta + base + 4 * BL * v, c[v] - p[v]);
+    stpol<SNT>(prev + base + 4 * BL * v, c[v]);
+  }
+}
+
 // Roofs: copy (1 in, 1 out) and 2-in-2-out with 512-lane blocks.
 template <int NV>
 __global__ __launch_bounds__(256) void copy_k(const float* a, float* b, long n) {
@@ -138,6 +181,29 @@ int main(int argc, char** argv) {
   float *c = g_cur, *p = g_prev, *d = g_delta;
   // every kernel below needs n to be a multiple of its tile
   if (n % 16384) { printf("n must be a multiple of 16384\n"); return 1; }
+  const bool policy = argc > 2 && atoi(argv[2]) == 1;
+  if (policy) {  // round 5: load / store policy, copy vs delta, interleaved twice
+    for (int rep = 0; rep < 2; ++rep) {
+      timeit("hipMemcpyAsync D2D", B8, [&] { CHECK(hipMemcpyAsync(d, c, n * 4, hipMemcpyDeviceToDevice, 0)); });
+      timeit("copy NV4 nt/nt", B8, [&] { copy_pol<4, true, true><<<n / 4096, 256>>>(c, d, n); });
+      timeit("copy NV4 nt/plain", B8, [&] { copy_pol<4, true, false><<<n / 4096, 256>>>(c, d, n); });
+      timeit("copy NV4 plain/nt", B8, [&] { copy_pol<4, false, true><<<n / 4096, 256>>>(c, d, n); });
+      timeit("copy NV4 plain/plain", B8, [&] { copy_pol<4, false, false><<<n / 4096, 256>>>(c, d, n); });
+      timeit("copy NV1 plain/plain", B8, [&] { copy_pol<1, false, false><<<n / 1024, 256>>>(c, d, n); });
+      timeit("copy gs x8/CU plain/plain", B8, [&] { copy_gs<false, false><<<cus * 8, 256>>>(c, d, n / 4); });
+      timeit("copy gs x32/CU plain/plain", B8, [&] { copy_gs<false, false><<<cus * 32, 256>>>(c, d, n / 4); });
+      timeit("copy gs x32/CU nt/nt", B8, [&] { copy_gs<true, true><<<cus * 32, 256>>>(c, d, n / 4); });
+      timeit("delta NV4 nt/nt (product)", B16, [&] { delta_pol<4, true, true, 256><<<n / 4096, 256>>>(c, p, d, n); });
+      timeit("delta NV4 nt/plain", B16, [&] { delta_pol<4, true, false, 256><<<n / 4096, 256>>>(c, p, d, n); });
+      timeit("delta NV4 plain/nt", B16, [&] { delta_pol<4, false, true, 256><<<n / 4096, 256>>>(c, p, d, n); });
+      timeit("delta NV4 plain/plain", B16, [&] { delta_pol<4, false, false, 256><<<n / 4096, 256>>>(c, p, d, n); });
+      timeit("delta512 NV2 nt/nt", B16, [&] { delta_pol<2, true, true, 512><<<n / 4096, 512>>>(c, p, d, n); });
+      timeit("delta512 NV2 nt/plain", B16, [&] { delta_pol<2, true, false, 512><<<n / 4096, 512>>>(c, p, d, n); });
+      timeit("delta NV1 nt/nt", B16, [&] { delta_pol<1, true, true, 256><<<n / 1024, 256>>>(c, p, d, n); });
+      timeit("delta NV2 nt/nt", B16, [&] { delta_pol<2, true, true, 256><<<n / 2048, 256>>>(c, p, d, n); });
+    }
+    return 0;
+  }
   for (int rep = 0; rep < 2; ++rep) {
     timeit("copy NV4", B8, [&] { copy_k<4><<<n / 4096, 256>>>(c, d, n); });
     timeit("copy NV8", B8, [&] { copy_k<8><<<n / 8192, 256>>>(c, d, n); });
