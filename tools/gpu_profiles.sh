@@ -24,19 +24,22 @@ run() {  # run <seconds> <log> <cmd...>
 F="--output-format csv"
 B="bench.py --no-sub --no-cpu-baseline --steps 2 --warmup 1"
 
+# ONLY="cfg3 delta ..." limits the traffic passes (and skips the SQ passes
+# unless one of their workloads is named); NO_STATS=1 skips the stats run.
 # kernel stats of the default bench (all sub-records), CPU baselines skipped
-run 600 "$OUT/stats_bench.log" rocprofv3 --kernel-trace --stats $F -d "$OUT/stats_bench" -o bench -- python3 -u bench.py --no-cpu-baseline
+[ -n "$NO_STATS" ] || run 600 "$OUT/stats_bench.log" rocprofv3 --kernel-trace --stats $F -d "$OUT/stats_bench" -o bench -- python3 -u bench.py --no-cpu-baseline
 
 # HBM traffic per launch: workload kernel coords peers [extra bench args]
 while IFS=: read -r w k c p extra; do
   [ -z "$w" ] && continue
+  [ -n "$ONLY" ] && [[ " $ONLY " != *" $w "* ]] && continue
   for cn in FETCH_SIZE WRITE_SIZE; do
     run 240 "$OUT/pmc_${cn}_$w.log" timeout -s KILL 220 rocprofv3 --pmc $cn $F -d "$OUT/pmc_${cn}_$w" -o run -- python3 -u $B $extra
   done
   python3 tools/pmc_traffic.py "$OUT/pmc_FETCH_SIZE_$w" "$OUT/pmc_WRITE_SIZE_$w" "$k" "$w" "$c" "$p" "$OUT/traffic_$w.json" > /dev/null || exit 1
 done <<'EOS'
-cfg3:fedavg_flat_kernel:125000000:256:--workload cfg3
-cfg3-chunk:fedavg_flat_kernel:15625000:256:--job cfg3-full --steps 1
+cfg3:fedavg_split_kernel+fedavg_flat_kernel:125000000:256:--workload cfg3
+cfg3-chunk:fedavg_split_kernel+fedavg_flat_kernel:15625000:256:--job cfg3-full --steps 1
 cfg2-dropin:fedavg_segments_kernel:11689512:64:--workload cfg2-dropin
 cfg4-median:robust_flat_kernel:100000000:128:--workload cfg4-median
 cfg4-trimmed:robust_flat_kernel:100000000:128:--workload cfg4-trimmed
@@ -47,6 +50,7 @@ EOS
 
 # issue / wait / clock counters of the K = 256 robust kernels (8 SQ + 2 GRBM slots)
 for w in median256 trimmed256 cfg4-median cfg4-trimmed; do
+  [ -n "$ONLY" ] && [[ " $ONLY " != *" $w "* ]] && continue
   run 240 "$OUT/pmc_sq_$w.log" timeout -s KILL 220 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT $F -d "$OUT/pmc_sq_$w" -o run -- python3 -u $B --workload $w
   python3 tools/rocpd_summary.py "$OUT/pmc_sq_$w" robust > "$OUT/sq_$w.json" || true
 done

@@ -20,21 +20,30 @@ import sys
 
 
 def per_dispatch(d, counter, kname):
+    """Per-launch value of `counter` for kernel-name substring kname.  kname
+    "a+b" (one aggregation call = launches of kernel a and of kernel b, e.g.
+    the split FedAvg kernel and the VGPR kernel over its remainder): every
+    matching dispatch is summed and divided by the dispatches of a."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
+    names = kname.split("+")
     vals = {}
+    first = set()
     for fn in files:
         with open(fn) as f:
             for row in csv.DictReader(f):
-                if row.get("Counter_Name") != counter or kname not in row.get("Kernel_Name", ""):
+                kn = row.get("Kernel_Name", "")
+                if row.get("Counter_Name") != counter or not any(x in kn for x in names):
                     continue
                 key = (fn, row.get("Dispatch_Id") or row.get("Correlation_Id"))
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    if not vals:
+                if names[0] in kn:
+                    first.add(key)
+    if not vals or not first:
         raise SystemExit(f"no {counter} rows for kernel '{kname}' in {d}")
     v = sorted(vals.values())
-    return v, sum(v) / len(v)
+    return v, sum(v) / len(first)
 
 
 def main():
