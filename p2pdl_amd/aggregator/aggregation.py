@@ -308,8 +308,12 @@ def _consuming(received):
     if len(inboxes) == 1:
         return next(iter(inboxes.values())).consuming()
     stack = contextlib.ExitStack()
-    for inbox in inboxes.values():
-        stack.enter_context(inbox.consuming())
+    try:
+        for inbox in inboxes.values():
+            stack.enter_context(inbox.consuming())
+    except BaseException:
+        stack.close()  # release the locks already taken
+        raise
     return stack
 
 

@@ -24,6 +24,8 @@
 // nontemporal loads (read once), one tile per block.  128 GB cfg3 tile:
 // 6.2-6.4 TB/s = 78-80% of 8 TB/s.  No inter-block reuse exists, so no XCD
 // remap is needed (guide T1: 0% on elementwise).
+#include <atomic>
+
 #include "p2p_common.h"
 
 namespace p2p {
@@ -325,17 +327,18 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* ag
 
 static int grid_for_tiles(int64_t ntiles) { return static_cast<int>(ntiles > 0 ? ntiles : 1); }
 
-// Compute units of the current device (cached per device id).
+// Compute units of the current device (cached per device id; concurrent
+// first calls store the same value).  Only the launch plan depends on it.
 static int device_cus() {
-  static int cus[64] = {0};
+  static std::atomic<int> cus[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cus[dev] == 0) {
-    int c = 0;
+  int c = cus[dev].load(std::memory_order_relaxed);
+  if (c == 0) {
     if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
-    cus[dev] = c;
+    cus[dev].store(c, std::memory_order_relaxed);
   }
-  return cus[dev];
+  return c;
 }
 
 // Flat launches.  With K >= kSplitMinK the split kernel takes whole ROUNDS of

@@ -1061,15 +1061,18 @@ class DeviceInbox:
         a message it does not accept raises ``pickle.UnpicklingError``.  The
         handle ``msg`` is consumed: its buffer returns to the pool once no
         window of it is alive (at once when none escapes)."""
-        if not isinstance(msg, PinnedMessage):  # pageable (over the pinned cap)
-            return _detached(decode_envelope(memoryview(msg).cast("B")))
         try:
-            obj = decode_envelope(msg.view())
-            if not (dict.get(obj, "type") == "model_update" and isinstance(dict.get(obj, "model"), memoryview)):
-                return _detached(obj)
-            return {k: (msg.window(v) if k == "model" else _detached(v)) for k, v in dict.items(obj)}
-        finally:
-            msg.release()
+            if not isinstance(msg, PinnedMessage):  # pageable (over the pinned cap)
+                return _detached(decode_envelope(memoryview(msg).cast("B")))
+            try:
+                obj = decode_envelope(msg.view())
+                if not (dict.get(obj, "type") == "model_update" and isinstance(dict.get(obj, "model"), memoryview)):
+                    return _detached(obj)
+                return {k: (msg.window(v) if k == "model" else _detached(v)) for k, v in dict.items(obj)}
+            finally:
+                msg.release()
+        except RecursionError as e:  # a nesting too deep, or a cycle (memo), to copy out
+            raise pickle.UnpicklingError("peer message nests too deeply") from e
 
     def _land_pinned_locked(self, msg: PinnedMessage, raw, k: int):
         """K5 device path: the message bytes in one DMA, then one landing

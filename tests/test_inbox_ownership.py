@@ -141,6 +141,26 @@ def test_no_envelope_reaches_an_unrestricted_unpickler(pageable, env, pinned, mo
     assert len(pageable.back) == (1 if pinned else 0)  # the buffer went back to the pool
 
 
+def test_cyclic_or_deep_envelope_is_an_unpickling_error(pageable):
+    """A self-referencing list (the machine's memo allows it) or a deep
+    nesting cannot escape as RecursionError from the copy-out."""
+    cyc = []
+    cyc.append(cyc)
+    deep = []
+    for _ in range(5000):
+        deep = [deep]
+    for obj in ({"type": "echo", "signature": cyc}, {"type": "ready", "sender_list": deep}):
+        import sys
+        lim = sys.getrecursionlimit()
+        sys.setrecursionlimit(max(lim, 20000))
+        try:
+            data = pickle.dumps(obj)
+        finally:
+            sys.setrecursionlimit(lim)
+        with pytest.raises(pickle.UnpicklingError):
+            open_envelope(message(pageable, data))
+
+
 def test_global_model_update_16bit_tensors_decode(pageable):
     """A float16 / bfloat16 global model decodes to the tensors pickle.loads
     gives (bit-equal, same dtype)."""
