@@ -22,7 +22,7 @@ run() {  # run <seconds> <log> <cmd...>
   [ $rc -eq 0 ] || { tail -30 "$logf"; exit $rc; }
 }
 F="--output-format csv"
-B="bench.py --no-sub --no-cpu-baseline --steps 2 --warmup 1"
+B="bench.py --no-sub --no-cpu-baseline --no-reference-gpu --steps 2 --warmup 1"
 
 # ONLY="cfg3 delta ..." limits the traffic passes (and skips the SQ passes
 # unless one of their workloads is named); NO_STATS=1 skips the stats run.
