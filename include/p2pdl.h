@@ -80,7 +80,12 @@ int64_t p2p_tile_elems(int32_t rule, int32_t k);
 /* ---- K1: FedAvg --------------------------------------------------------
  * Replaces reference aggregator/aggregation.py:15-38 for one flat buffer:
  *   acc = +0 (:15); acc += peers[j] for j in list order (:25-28);
- *   acc /= K (:31-32); w += fp32(lr) * acc (:36-38, lr = 0.1 there). */
+ *   acc /= K (:31-32); w += fp32(lr) * acc (:36-38, lr = 0.1 there).
+ * Kernel choice (a pure function of k and n, same bits either way): for
+ * k >= 16, whole rounds of 8192-float tiles (a multiple of the CU count) run
+ * on the LDS-DMA split kernel (loader + consumer waves), the rest on the
+ * VGPR kernel.  The peer pointers are read from device memory each launch;
+ * 4-byte-aligned (not 16-byte) pointers are handled, more slowly. */
 int32_t p2p_fedavg_apply_f32(const float *const *peers, int32_t k, int64_t n, float *w, float lr,
                              p2p_stream_t stream);
 /* Same reduction, writes acc/K to out (the :15-32 part, no apply). */
