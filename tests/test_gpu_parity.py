@@ -199,6 +199,8 @@ def split_expect(k, seed, a, b, torch_gpu=False, kk=None):
     (16, SPLIT_MIN_TILES * SPLIT_TILE + 4099, "fedavg"),   # smallest split K, ragged tail with a partial float4
     (64, SPLIT_MIN_TILES * SPLIT_TILE, "fedavg_torch_gpu"),  # no tail; torch's GPU division form
     (256, 1907 * SPLIT_TILE + 4097 + 3, "fedavg"),         # cfg3's K and its 8-GPU chunk: 7 rounds + 115 tiles + tail
+    (17, 512 * SPLIT_TILE + 101, "fedavg"),                # odd K; two rounds on 256 CUs + a 101-float tail
+    (255, 256 * SPLIT_TILE, "fedavg_torch_gpu"),           # one round exactly, no VGPR remainder
 ])
 def test_fedavg_split_kernel_vs_oracle(cuda, k, n, rule):
     seed = 0x5B17 + k
