@@ -38,8 +38,10 @@ extern "C" {
  * 4: adds the rule P2P_RULE_FEDAVG_TORCH_GPU and p2p_fedavg_apply_16
  *    (float16 / bfloat16 models).
  * 5: P2P_DELTA_TILE 4096 -> 1024 (the delta segment table's tile_begin is
- *    counted in 1024-element tiles). */
-#define P2P_ABI_VERSION 5
+ *    counted in 1024-element tiles).
+ * 6: adds p2p_fedavg_split_plan / p2p_fedavg_split_segments_f32 (whole
+ *    tiles of a state_dict on the LDS-DMA split kernel). */
+#define P2P_ABI_VERSION 6
 
 typedef void *p2p_stream_t; /* hipStream_t */
 
@@ -115,6 +117,25 @@ int32_t p2p_trimmed_mean_f32(const float *const *peers, int32_t k, int64_t n, in
  * w, out must be non-null).  trim_b is read only for P2P_RULE_TRIMMED. */
 int32_t p2p_aggregate_f32(const float *const *peers, int32_t k, int64_t n, int32_t rule,
                           int32_t trim_b, float lr, float *w, float *out, p2p_stream_t stream);
+
+/* The LDS-DMA split kernel over whole P2P_SPLIT_TILE-element tiles of a
+ * segment table (FedAvg rules only): entry t of the DEVICE array `tiles`
+ * names segment `seg` of `segs` and the tile's first element `c0` in it.
+ * Precondition (the caller's, checked where the list is built): every listed
+ * segment's K peer pointers and w / out are 16-byte aligned and
+ * c0 + P2P_SPLIT_TILE <= n.  The rest of each segment goes through
+ * p2p_aggregate_segments_f32 (a table of the remaining ranges).
+ * p2p_fedavg_split_plan(k, full) is how many of `full` whole tiles to list:
+ * whole rounds of the device's CU count, 0 for k < 16 (same results either
+ * way; the plan is speed only). */
+#define P2P_SPLIT_TILE 8192
+typedef struct p2p_split_tile_t {
+  int64_t seg; /* index into segs */
+  int64_t c0;  /* first element of the tile inside the segment */
+} p2p_split_tile_t;
+int64_t p2p_fedavg_split_plan(int32_t k, int64_t full_tiles);
+int32_t p2p_fedavg_split_segments_f32(const p2p_split_tile_t *tiles, int64_t ntiles, const p2p_segment_t *segs,
+                                      int32_t k, int32_t rule, float lr, p2p_stream_t stream);
 
 /* Whole state_dict in ONE launch: segs is a DEVICE array of nseg entries
  * (tile_begin prefix-summed with p2p_tile_elems(rule, k)); total_tiles is the

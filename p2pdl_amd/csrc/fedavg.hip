@@ -224,17 +224,45 @@ __device__ __forceinline__ void lds_read4(f4 (&x)[4], uint32_t a) {
       : "v"(a));
 }
 
-template <bool RECIP>
+// Where split tile t lives: a flat buffer (tile t at t * kSTile), or (SEGS)
+// entry t of a host-built tile list naming a segment of a state_dict table
+// and the tile's first element in it.  Wave-uniform (scalar loads).
+struct SplitTile {
+  const float* const* peers;
+  float* w;
+  float* out;
+  int64_t c0;
+};
+template <bool SEGS>
+__device__ __forceinline__ SplitTile split_tile(const float* const* peers, float* w, float* out,
+                                                const p2p_split_tile_t* tiles, const Seg* segs, int64_t t) {
+  if constexpr (SEGS) {
+    const int64_t seg = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&tiles[t].seg))));
+    const int64_t c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&tiles[t].c0))));
+    const Seg* sp = segs + seg;
+    return SplitTile{reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->peers)))),
+                     reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->w)))),
+                     reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->out)))), c0};
+  } else {
+    return SplitTile{peers, w, out, t * kSTile};
+  }
+}
+
+// SEGS: the host lists only whole tiles of segments whose K peer pointers and
+// w / out are all 16-B aligned (ops.py checks them when it builds the list);
+// a flat buffer is checked here.
+template <bool RECIP, bool SEGS>
 __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const float* const* __restrict__ peers,
                                                                         int K, const int32_t* k_dev,
                                                                         int64_t ntiles, float* w, float* out,
-                                                                        float lr) {
+                                                                        float lr, const p2p_split_tile_t* tiles,
+                                                                        const Seg* segs) {
   __shared__ __attribute__((aligned(16))) float lds[(kSS + 1) * kSTile];
   if (k_dev) K = __builtin_amdgcn_readfirstlane(ldg(k_dev));
   if (K <= 0) return;
   const int64_t G = gridDim.x, b = bid_x();
   const int wv = __builtin_amdgcn_readfirstlane(tid_x() >> 6), lane = tid_x() & 63;
-  if (!all_aligned16(peers, K, w, out)) {
+  if (!SEGS && !all_aligned16(peers, K, w, out)) {
     // 4-B-aligned views: element-wise, same op order, no LDS (block-uniform)
     for (int64_t t = b; t < ntiles; t += G)
       for (int e = tid_x(); e < kSTile; e += 64 * (kSL + kSC))
@@ -245,8 +273,10 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
   if (wv < kSL) {
     int64_t ti = b, issued = 0;
     int ki = 0, si = 0;
+    SplitTile tl = split_tile<SEGS>(peers, w, out, tiles, segs, ti);
     auto issue = [&]() {
-      const float* src = table_at(peers, ki) + ti * kSTile + (wv * kSPer) * 256 + lane * 4;
+      if (ki == 0 && issued > 0) tl = split_tile<SEGS>(peers, w, out, tiles, segs, ti);
+      const float* src = table_at(tl.peers, ki) + tl.c0 + (wv * kSPer) * 256 + lane * 4;
 #pragma unroll
       for (int q = 0; q < kSPer; ++q) dma16<2 /* nt */>(src + q * 256, &lds[si * kSTile + (wv * kSPer + q) * 256]);
       ++issued;
@@ -269,10 +299,11 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
   const float inv = RECIP ? 1.0f / fk : 0.f;
   int slot = 0;
   for (int64_t t = b; t < ntiles; t += G) {
-    const int64_t o = t * kSTile + cw * kSRpw * 256 + lane * 4;
-    if (w) {
+    const SplitTile tl = split_tile<SEGS>(peers, w, out, tiles, segs, t);
+    const int64_t o = tl.c0 + cw * kSRpw * 256 + lane * 4;
+    if (tl.w) {
 #pragma unroll
-      for (int r = 0; r < kSRpw; ++r) dma16<0>(w + o + r * 256, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
+      for (int r = 0; r < kSRpw; ++r) dma16<0>(tl.w + o + r * 256, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
     }
     f4 acc[kSRpw];
 #pragma unroll
@@ -288,16 +319,16 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
     f4 m[kSRpw];
 #pragma unroll
     for (int r = 0; r < kSRpw; ++r) m[r] = div4<RECIP>(acc[r], fk, inv);  // (:31-32)
-    if (out) {
+    if (tl.out) {
 #pragma unroll
-      for (int r = 0; r < kSRpw; ++r) st(out + o + r * 256, m[r]);
+      for (int r = 0; r < kSRpw; ++r) st(tl.out + o + r * 256, m[r]);
     }
-    if (w) {
+    if (tl.w) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w DMA (and its older stores)
       f4 wq[kSRpw];
       lds_read4(wq, lds0 + static_cast<uint32_t>(kSS * kSTile * 4) + mine);
 #pragma unroll
-      for (int r = 0; r < kSRpw; ++r) st(w + o + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
+      for (int r = 0; r < kSRpw; ++r) st(tl.w + o + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
     }
   }
 }
@@ -349,21 +380,37 @@ static int device_cus() {
 // 8 split rounds would leave half the CUs idle in the last one.  The grid is
 // CUs x R blocks with R the largest divisor of the round count <= 8 (equal
 // tiles per block).  K is the kernarg or, for the device-K path, k_max.
+// Split tiles for `full` whole tiles: whole rounds of the CU count (0 below
+// one round or for K < kSplitMinK).
+static int64_t split_tiles_for(int K, int64_t full) {
+  if (K < kSplitMinK || full <= 0) return 0;
+  const int64_t cus = device_cus();
+  return full / cus * cus;
+}
+// CUs x R blocks, R the largest divisor of the round count <= 8 (a tile
+// count that is not whole rounds -- a caller's own list -- still runs, one
+// block per tile up to that grid).
+static dim3 split_grid(int64_t tiles) {
+  const int64_t cus = device_cus(), rounds = tiles / cus;
+  if (rounds < 1) return dim3(static_cast<unsigned>(tiles));
+  int64_t r = kSRoundsPerBlockMax < rounds ? kSRoundsPerBlockMax : rounds;
+  while (r > 1 && rounds % r) --r;
+  return dim3(static_cast<unsigned>(cus * r));
+}
+
 static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,
                         float lr, hipStream_t stream, bool recip = false) {
   int64_t done = 0;
-  if (K >= kSplitMinK) {
-    const int64_t cus = device_cus();
-    const int64_t rounds = n / kSTile / cus;
-    if (rounds >= 1) {
-      int64_t r = kSRoundsPerBlockMax < rounds ? kSRoundsPerBlockMax : rounds;
-      while (rounds % r) --r;
-      const int64_t tiles = rounds * cus;
-      const dim3 grid(static_cast<unsigned>(cus * r)), block(64 * (kSL + kSC));
+  {
+    const int64_t tiles = split_tiles_for(K, n / kSTile);
+    if (tiles > 0) {
+      const dim3 grid = split_grid(tiles), block(64 * (kSL + kSC));
       if (recip)
-        hipLaunchKernelGGL(fedavg_split_kernel<true>, grid, block, 0, stream, peers, K, k_dev, tiles, w, out, lr);
+        hipLaunchKernelGGL((fedavg_split_kernel<true, false>), grid, block, 0, stream, peers, K, k_dev, tiles, w, out,
+                           lr, nullptr, nullptr);
       else
-        hipLaunchKernelGGL(fedavg_split_kernel<false>, grid, block, 0, stream, peers, K, k_dev, tiles, w, out, lr);
+        hipLaunchKernelGGL((fedavg_split_kernel<false, false>), grid, block, 0, stream, peers, K, k_dev, tiles, w, out,
+                           lr, nullptr, nullptr);
       done = tiles * kSTile;
       if (done == n) return;
     }
@@ -394,6 +441,27 @@ static int32_t launch_status() {
 }
 
 extern "C" P2P_INTERNAL int64_t p2p_fedavg_tile_elems(void) { return kTile; }
+
+static_assert(kSTile == P2P_SPLIT_TILE, "the ABI's split tile");
+
+extern "C" int64_t p2p_fedavg_split_plan(int32_t k, int64_t full_tiles) { return split_tiles_for(k, full_tiles); }
+
+extern "C" int32_t p2p_fedavg_split_segments_f32(const p2p_split_tile_t* tiles, int64_t ntiles,
+                                                 const p2p_segment_t* segs, int32_t k, int32_t rule, float lr,
+                                                 p2p_stream_t stream) {
+  if (!tiles || !segs || k < 1 || ntiles < 0) return P2P_ERR_INVALID;
+  if (rule != P2P_RULE_FEDAVG && rule != P2P_RULE_FEDAVG_TORCH_GPU) return P2P_ERR_INVALID;
+  if (ntiles == 0) return P2P_OK;
+  const dim3 grid = split_grid(ntiles), block(64 * (kSL + kSC));
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  if (rule == P2P_RULE_FEDAVG_TORCH_GPU)
+    hipLaunchKernelGGL((fedavg_split_kernel<true, true>), grid, block, 0, st, nullptr, k, nullptr, ntiles, nullptr,
+                       nullptr, lr, tiles, segs);
+  else
+    hipLaunchKernelGGL((fedavg_split_kernel<false, true>), grid, block, 0, st, nullptr, k, nullptr, ntiles, nullptr,
+                       nullptr, lr, tiles, segs);
+  return launch_status();
+}
 
 P2P_INTERNAL int32_t p2p_fedavg_flat_launch(const float* const* peers, int32_t k, int64_t n, float* w,
                                             float* out, float lr, p2p_stream_t stream, int32_t recip) {

@@ -247,6 +247,37 @@ def _launch_table(base: int, L: int, tiles: int, K: int, r: int, b: int, lr: flo
             "p2p_aggregate_segments_f32")
 
 
+SPLIT_TILE = 8192  # == P2P_SPLIT_TILE
+_SPLIT_DTYPE = np.dtype([("seg", "<i8"), ("c0", "<i8")])  # == p2p_split_tile_t (16 B)
+
+
+def _split_plan(ptrs: np.ndarray, w_ptrs, out_ptrs, n_arr: np.ndarray, K: int, r: int):
+    """FedAvg over a state_dict: which whole 8192-element tiles go to the
+    LDS-DMA split kernel (include/p2pdl.h p2p_fedavg_split_segments_f32).
+    Whole tiles of segments whose K peer pointers and w / out are 16-B
+    aligned, taken in segment order, as many as p2p_fedavg_split_plan allows
+    (whole rounds of the CU count).  Returns (taken tiles per segment, the
+    split list) or None when nothing goes to the split kernel."""
+    if r not in FEDAVG_RULES or K < 16:
+        return None
+    full = n_arr // SPLIT_TILE
+    aligned = (ptrs % np.uint64(16) == 0).all(axis=1) & (np.asarray(w_ptrs, dtype=np.uint64) % np.uint64(16) == 0)
+    if out_ptrs is not None:
+        aligned &= np.asarray(out_ptrs, dtype=np.uint64) % np.uint64(16) == 0
+    full = np.where(aligned, full, 0)
+    S = int(N.lib().p2p_fedavg_split_plan(K, int(full.sum())))
+    if S <= 0:
+        return None
+    before = np.cumsum(full) - full
+    taken = np.clip(S - before, 0, full)
+    seg = np.repeat(np.arange(len(n_arr), dtype=np.int64), taken)
+    first = np.repeat(np.cumsum(taken) - taken, taken)
+    lst = np.empty(S, dtype=_SPLIT_DTYPE)
+    lst["seg"] = seg
+    lst["c0"] = (np.arange(S, dtype=np.int64) - first) * SPLIT_TILE
+    return taken, lst
+
+
 def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_frac, outs, dev, cache_key=None):
     r = rule_id(rule)
     if r not in FEDAVG_RULES and K > MAX_ROBUST_PEERS:
@@ -254,38 +285,83 @@ def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_fra
     b = trim_count(K, trim_frac) if (r == P2P_RULE_TRIMMED and trim_b is None) else int(trim_b or 0)
     tile = int(N.lib().p2p_tile_elems(r, K))
     L = len(ws)
-    segs = np.zeros(L, dtype=_SEG_DTYPE)
     n_arr = np.asarray(numels, dtype=np.int64)
-    segs["w"] = [w.data_ptr() for w in ws]
+    w_ptrs = [w.data_ptr() for w in ws]
+    out_ptrs = [o.data_ptr() for o in outs] if outs is not None else None
+    ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+    plan = _split_plan(ptrs, w_ptrs, out_ptrs, n_arr, K, r)
+    # The table the VGPR segment kernel runs: every segment, or -- with a
+    # split plan -- what the split kernel leaves of each (its tail past the
+    # taken whole tiles), as segments of their own whose peer rows, w and out
+    # start at that offset.
+    if plan is None:
+        rem_idx, start = np.arange(L), np.zeros(L, dtype=np.int64)
+    else:
+        taken = plan[0]
+        start = taken * SPLIT_TILE
+        rem_idx = np.nonzero(n_arr - start > 0)[0]
+        start = start[rem_idx]
+    Lr = len(rem_idx)
+    rem = np.zeros(Lr, dtype=_SEG_DTYPE)
+    rem["w"] = np.asarray(w_ptrs, dtype=np.uint64)[rem_idx] + start.astype(np.uint64) * np.uint64(4)
     if outs is not None:
-        segs["out"] = [o.data_ptr() for o in outs]
-    segs["n"] = n_arr
-    t_arr = -(-n_arr // tile)
-    segs["tile_begin"][1:] = np.cumsum(t_arr)[:-1]
+        rem["out"] = np.asarray(out_ptrs, dtype=np.uint64)[rem_idx] + start.astype(np.uint64) * np.uint64(4)
+    rem["n"] = n_arr[rem_idx] - start
+    t_arr = -(-rem["n"] // tile)
+    if Lr:
+        rem["tile_begin"][1:] = np.cumsum(t_arr)[:-1]
     tiles = int(t_arr.sum())
-    if tiles == 0:
+    rem_ptrs = ptrs[rem_idx] + (start.astype(np.uint64) * np.uint64(4))[:, None]
+    if tiles == 0 and plan is None:
         return
-    seg_bytes = segs.nbytes
-    # the table holds device addresses inside itself (segment l -> its row of
-    # K peer pointers): allocate the device buffer first, then fill the host
-    # image with those addresses and copy it once
-    host = np.empty(seg_bytes + ptrs.nbytes, dtype=np.uint8)
-    host[seg_bytes:] = np.ascontiguousarray(ptrs, dtype=np.uint64).view(np.uint8).reshape(-1)
+    # one device buffer: [the full table (split kernel's segments)] [the
+    # remainder table] [split tile list] [full peer rows] [remainder peer
+    # rows].  Its tables hold device addresses inside itself: allocate it
+    # first, then fill the host image with those addresses and copy it once.
+    full = np.zeros(L if plan is not None else 0, dtype=_SEG_DTYPE)
+    lst = plan[1] if plan is not None else np.zeros(0, dtype=_SPLIT_DTYPE)
+    parts = [full.nbytes, rem.nbytes, lst.nbytes, 8 * K * len(full), rem_ptrs.nbytes]
+    offs = np.concatenate([[0], np.cumsum(parts)]).astype(np.int64)
+    host = np.empty(int(offs[-1]), dtype=np.uint8)
     buf = torch.empty(host.nbytes, dtype=torch.uint8, device=dev)
     base = buf.data_ptr()
-    segs["peers"] = np.uint64(base + seg_bytes) + np.arange(L, dtype=np.uint64) * np.uint64(8 * K)
-    host[:seg_bytes] = segs.view(np.uint8)
+    if plan is not None:
+        full["w"] = w_ptrs
+        if outs is not None:
+            full["out"] = out_ptrs
+        full["n"] = n_arr
+        full["peers"] = np.uint64(base + offs[3]) + np.arange(L, dtype=np.uint64) * np.uint64(8 * K)
+        host[offs[0]:offs[1]] = full.view(np.uint8)
+        host[offs[2]:offs[3]] = lst.view(np.uint8)
+        host[offs[3]:offs[4]] = ptrs.view(np.uint8).reshape(-1)
+    rem["peers"] = np.uint64(base + offs[4]) + np.arange(Lr, dtype=np.uint64) * np.uint64(8 * K)
+    host[offs[1]:offs[2]] = rem.view(np.uint8)
+    host[offs[4]:offs[5]] = rem_ptrs.view(np.uint8).reshape(-1)
     _RING.to_device(host, dev, out=buf)
+    split = None if plan is None else (int(offs[2]), len(lst), int(offs[0]))
+    entry = (buf, tiles, r, b, torch.cuda.current_stream(dev).cuda_stream, (int(offs[1]), Lr, split))
     with torch.cuda.device(dev):
-        _launch_table(base, L, tiles, K, r, b, lr)
+        _launch_entry(entry, K, lr, N.stream_handle())
     if cache_key is not None:
-        entry = (buf, tiles, r, b, torch.cuda.current_stream(dev).cuda_stream)
         with _TABLES_LOCK:
             _TABLES[cache_key] = entry
             while len(_TABLES) > _TABLES_MAX:
                 _TABLES.popitem(last=False)
         return entry
     return None
+
+
+def _launch_entry(entry, K: int, lr: float, stream) -> None:
+    """The launches of one segment-table entry: the split kernel over its
+    tile list (when planned), then the VGPR segment kernel over the rest."""
+    buf, tiles, r, b, _, (rem_off, Lr, split) = entry
+    base = buf.data_ptr()
+    if split is not None:
+        lst_off, S, segs_off = split
+        N.check(N.lib().p2p_fedavg_split_segments_f32(base + lst_off, S, base + segs_off, K, r, lr, stream),
+                "p2p_fedavg_split_segments_f32")
+    if tiles:
+        _launch_table(base + rem_off, Lr, tiles, K, r, b, lr, stream=stream)
 
 
 def aggregate_segments_(ws: Sequence[torch.Tensor], peer_lists: Sequence[Sequence[torch.Tensor]],
@@ -361,12 +437,7 @@ def aggregate_ptr_table_(ws: Sequence[torch.Tensor], ptrs: np.ndarray, rule="fed
         if hit is not None:
             _TABLES.move_to_end(key)
     if hit is not None:
-        buf, tiles, r, b, alloc_stream = hit
-        with torch.cuda.device(dev) if torch.cuda.current_device() != dev.index else _NO_CTX:
-            raw = N.stream_handle(dev)
-            if raw != alloc_stream:
-                buf.record_stream(torch.cuda.current_stream(dev))
-            _launch_table(buf.data_ptr(), L, tiles, K, r, b, lr, stream=raw)
+        _relaunch(hit, dev, K, lr)
         return
     _launch_segments(ws, ptrs, numels, rule, K, lr, trim_b, trim_frac, None, dev, cache_key=key)
 
@@ -428,12 +499,16 @@ def relaunch(entry, dev, L: int, K: int, lr: float) -> None:
     over the same addresses, on the current stream of ``dev`` -- no table
     work, no H2D copy, no per-call checks (the caller vouches that the
     addresses it was built from are unchanged)."""
-    buf, tiles, r, b, alloc_stream = entry
+    _relaunch(entry, dev, K, lr)
+
+
+def _relaunch(entry, dev, K: int, lr: float) -> None:
+    buf, alloc_stream = entry[0], entry[4]
     with torch.cuda.device(dev) if torch.cuda.current_device() != dev.index else _NO_CTX:
         raw = N.stream_handle(dev.index)
         if raw != alloc_stream:
             buf.record_stream(torch.cuda.current_stream(dev))  # eviction must not recycle it under this launch
-        _launch_table(buf.data_ptr(), L, tiles, K, r, b, lr, stream=raw)
+        _launch_entry(entry, K, lr, raw)
 
 
 # ------------------------------------------------------------------ K4

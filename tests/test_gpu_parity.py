@@ -240,6 +240,56 @@ def test_fedavg_split_kernel_devk(cuda):
         assert_bits_equal(got[a:b], split_expect(k, seed, a, b)[0], what=f"devk [{a}, {b})")
 
 
+@pytest.mark.parametrize("k,rule,with_out", [(20, "fedavg", False), (64, "fedavg_torch_gpu", True)])
+def test_fedavg_split_segments_vs_oracle(cuda, k, rule, with_out):
+    """A state_dict through the split kernel's tile list (ops._split_plan:
+    whole 8192-element tiles of aligned segments, whole CU rounds) and the
+    VGPR segment kernel over the rest -- segments of every size class, one
+    segment whose peer views are only 4-B aligned (left out of the list) --
+    bit-exact against the oracle, segment by segment."""
+    sizes = [2_500_001, 100, 8191, 8192, 700_001, 1_234_567, 3, 300_000]
+    seed = 0x5E65 + k
+    ws, peer_lists, outs, want_w, want_o = [], [[] for _ in range(k)], [], [], []
+    for l, n in enumerate(sizes):
+        misaligned = l == 5
+        raw = torch.empty((k, n + 8), dtype=torch.float32, device=cuda)
+        for p in range(k):
+            ops.fill_synthetic_(raw[p], seed + l, p, 1e-2)
+        views = [raw[p, 1:1 + n] if misaligned else raw[p, :n] for p in range(k)]
+        for p in range(k):
+            peer_lists[p].append(views[p])
+        w = torch.empty(n, dtype=torch.float32, device=cuda)
+        ops.fill_synthetic_(w, seed + l, 0xFFFFF, 5e-2)
+        host_peers = [v.cpu().numpy() for v in views]
+        wr, orr = oracle.fedavg(host_peers, w.cpu().numpy(), want_out=True, torch_gpu=rule == "fedavg_torch_gpu")
+        ws.append(w)
+        outs.append(torch.empty(n, dtype=torch.float32, device=cuda))
+        want_w.append(wr)
+        want_o.append(orr)
+    ops.aggregate_segments_(ws, peer_lists, rule, outs=outs if with_out else None)
+    for l in range(len(sizes)):
+        assert_bits_equal(host(ws[l]), want_w[l], what=f"segment {l} w")
+        if with_out:
+            assert_bits_equal(host(outs[l]), want_o[l], what=f"segment {l} mean")
+
+
+def test_split_plan_takes_whole_rounds_of_aligned_tiles(cuda):
+    """The plan itself (host logic): whole tiles of aligned segments only, in
+    segment order, whole rounds of the CU count; each segment's rest is its
+    tail for the VGPR kernel."""
+    K, cus = 32, torch.cuda.get_device_properties(cuda).multi_processor_count
+    n_arr = np.array([5 * 8192 + 7, (cus + 44) * 8192, 40 * 8192, 10], dtype=np.int64)
+    ptrs = np.full((4, K), 1 << 20, dtype=np.uint64)
+    ptrs[2, 3] += 4  # segment 2: one peer view only 4-B aligned
+    taken, lst = ops._split_plan(ptrs, [1 << 24] * 4, None, n_arr, K, 0)
+    assert len(lst) == cus and int(taken.sum()) == cus  # 5 + cus + 44 whole aligned tiles -> one round
+    assert list(taken) == [5, cus - 5, 0, 0]
+    assert list(lst["seg"][:6]) == [0] * 5 + [1] and list(lst["c0"][:6]) == [0, 8192, 16384, 24576, 32768, 0]
+    assert ops._split_plan(ptrs, [1 << 24] * 4, None, n_arr, 15, 0) is None  # K < 16
+    assert ops._split_plan(ptrs, [1 << 24] * 4, None, n_arr, K, 1) is None   # median
+    assert ops._split_plan(ptrs[:, :], [(1 << 24) + 8] * 4, None, n_arr, K, 0) is None  # w misaligned everywhere
+
+
 def resnet18_param_shapes():
     """The 62 parameter tensors of torchvision's ResNet-18 (11,689,512
     params, BASELINE cfg2), in state_dict order."""
