@@ -248,6 +248,13 @@ def _launch_table(base: int, L: int, tiles: int, K: int, r: int, b: int, lr: flo
 
 
 SPLIT_TILE = 8192  # == P2P_SPLIT_TILE
+# A state_dict goes to the split kernel only when its plan covers at least
+# this many whole tiles (67M coordinates).  Same-box A/B (tools/seg_ab.py, K =
+# 64, profiles/r05/seg): at ResNet-18's 11.7M coordinates (1280 planned tiles)
+# split + segments ran 0.4-1.7% SLOWER than the VGPR segment kernel alone on
+# three boxes -- the second launch over each tensor's ragged rest costs what
+# the split tiles save; at 4x those shapes (5632 tiles) +0.9%, at 16x +2.5%.
+SPLIT_SEGMENT_MIN_TILES = 2048
 _SPLIT_DTYPE = np.dtype([("seg", "<i8"), ("c0", "<i8")])  # == p2p_split_tile_t (16 B)
 
 
@@ -256,7 +263,8 @@ def _split_plan(ptrs: np.ndarray, w_ptrs, out_ptrs, n_arr: np.ndarray, K: int, r
     LDS-DMA split kernel (include/p2pdl.h p2p_fedavg_split_segments_f32).
     Whole tiles of segments whose K peer pointers and w / out are 16-B
     aligned, taken in segment order, as many as p2p_fedavg_split_plan allows
-    (whole rounds of the CU count).  Returns (taken tiles per segment, the
+    (whole rounds of the CU count), if that is SPLIT_SEGMENT_MIN_TILES or
+    more.  Returns (taken tiles per segment, the
     split list) or None when nothing goes to the split kernel."""
     if r not in FEDAVG_RULES or K < 16:
         return None
@@ -266,7 +274,7 @@ def _split_plan(ptrs: np.ndarray, w_ptrs, out_ptrs, n_arr: np.ndarray, K: int, r
         aligned &= np.asarray(out_ptrs, dtype=np.uint64) % np.uint64(16) == 0
     full = np.where(aligned, full, 0)
     S = int(N.lib().p2p_fedavg_split_plan(K, int(full.sum())))
-    if S <= 0:
+    if S <= 0 or S < SPLIT_SEGMENT_MIN_TILES:
         return None
     before = np.cumsum(full) - full
     taken = np.clip(S - before, 0, full)

@@ -241,12 +241,13 @@ def test_fedavg_split_kernel_devk(cuda):
 
 
 @pytest.mark.parametrize("k,rule,with_out", [(20, "fedavg", False), (64, "fedavg_torch_gpu", True)])
-def test_fedavg_split_segments_vs_oracle(cuda, k, rule, with_out):
+def test_fedavg_split_segments_vs_oracle(cuda, k, rule, with_out, monkeypatch):
     """A state_dict through the split kernel's tile list (ops._split_plan:
     whole 8192-element tiles of aligned segments, whole CU rounds) and the
     VGPR segment kernel over the rest -- segments of every size class, one
     segment whose peer views are only 4-B aligned (left out of the list) --
     bit-exact against the oracle, segment by segment."""
+    monkeypatch.setattr(ops, "SPLIT_SEGMENT_MIN_TILES", 0)  # these sizes sit below the product's gate
     sizes = [2_500_001, 100, 8191, 8192, 700_001, 1_234_567, 3, 300_000]
     seed = 0x5E65 + k
     ws, peer_lists, outs, want_w, want_o = [], [[] for _ in range(k)], [], [], []
@@ -273,7 +274,29 @@ def test_fedavg_split_segments_vs_oracle(cuda, k, rule, with_out):
             assert_bits_equal(host(outs[l]), want_o[l], what=f"segment {l} mean")
 
 
-def test_split_plan_takes_whole_rounds_of_aligned_tiles(cuda):
+def test_fedavg_split_segments_at_the_product_gate(cuda):
+    """Default gate: a 16-peer state_dict with SPLIT_SEGMENT_MIN_TILES whole
+    tiles and more goes through the split plan, bit-exact on every tensor."""
+    k, rule, seed = 16, "fedavg", 0x5E70
+    sizes = [9_000_001, 8_200_000 + 5, 100]
+    plan_tiles = sum(n // SPLIT_TILE for n in sizes)
+    assert int(ops.N.lib().p2p_fedavg_split_plan(k, plan_tiles)) >= ops.SPLIT_SEGMENT_MIN_TILES
+    ws, peer_lists, want = [], [[] for _ in range(k)], []
+    for l, n in enumerate(sizes):
+        raw = torch.empty((k, n + 64), dtype=torch.float32, device=cuda)
+        for p in range(k):
+            ops.fill_synthetic_(raw[p], seed + l, p, 1e-2)
+            peer_lists[p].append(raw[p, :n])
+        w = torch.empty(n, dtype=torch.float32, device=cuda)
+        ops.fill_synthetic_(w, seed + l, 0xFFFFF, 5e-2)
+        want.append(oracle.fedavg([host(raw[p, :n]) for p in range(k)], host(w))[0])
+        ws.append(w)
+    ops.aggregate_segments_(ws, peer_lists, rule)
+    for l in range(len(sizes)):
+        assert_bits_equal(host(ws[l]), want[l], what=f"segment {l} w")
+
+
+def test_split_plan_takes_whole_rounds_of_aligned_tiles(cuda, monkeypatch):
     """The plan itself (host logic): whole tiles of aligned segments only, in
     segment order, whole rounds of the CU count; each segment's rest is its
     tail for the VGPR kernel."""
@@ -281,6 +304,8 @@ def test_split_plan_takes_whole_rounds_of_aligned_tiles(cuda):
     n_arr = np.array([5 * 8192 + 7, (cus + 44) * 8192, 40 * 8192, 10], dtype=np.int64)
     ptrs = np.full((4, K), 1 << 20, dtype=np.uint64)
     ptrs[2, 3] += 4  # segment 2: one peer view only 4-B aligned
+    assert ops._split_plan(ptrs, [1 << 24] * 4, None, n_arr, K, 0) is None  # under SPLIT_SEGMENT_MIN_TILES
+    monkeypatch.setattr(ops, "SPLIT_SEGMENT_MIN_TILES", 0)
     taken, lst = ops._split_plan(ptrs, [1 << 24] * 4, None, n_arr, K, 0)
     assert len(lst) == cus and int(taken.sum()) == cus  # 5 + cus + 44 whole aligned tiles -> one round
     assert list(taken) == [5, cus - 5, 0, 0]
