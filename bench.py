@@ -60,7 +60,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from p2pdl_amd import ops  # noqa: E402
+from p2pdl_amd import ops, sharded  # noqa: E402
 
 METRIC = "aggregated peer-update GB/s (% HBM peak) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
@@ -243,21 +243,24 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
     """Resident [K, n] slab per rank; a step = the rule over it (+ the chunked
     all-gather at N > 1).  Returns (record, ms_per_step)."""
     world, rank, dev = c.world, c.rank, c.dev
-    S = chunks if world > 1 else 1
-    C = -(-n // S)
-    n = C * S  # whole chunks per rank
+    # the product's memory-sharded layout (sharded.PeerPlanes): chunk-major
+    # planes of K rows spanning <= 16 GB each, at least the all-gather
+    # pipeline's chunks at N > 1
+    S = sharded.plane_count(K, n, at_least=chunks if world > 1 else 1)
+    C = n // S
     free, _ = torch.cuda.mem_get_info(dev)
     need = (K + 2 + world) * n * 4
     if need > free * 0.97:
         raise SystemExit(f"{name}: needs {need/1e9:.1f} GB, {free/1e9:.1f} GB free")
-    log(f"[rank {rank}] {name}: generating {K} x {n:,} fp32 peer slab ({K*n*4/1e9:.1f} GB)")
-    slab, w = pitched_slab(K, S, C, dev), pitched_slab(1, S, C, dev)[0]
+    log(f"[rank {rank}] {name}: generating {K} x {n:,} fp32 peer data ({K*n*4/1e9:.1f} GB) "
+        f"as {S} plane(s) of {K} x {C:,}")
+    planes, w = sharded.PeerPlanes(K, S, C, dev), pitched_slab(1, S, C, dev)[0]
     for s in range(S):  # local chunk s is global chunk s*N + rank
         for p in range(K):
-            ops.fill_synthetic_(slab[p, s, :C], seed, p, UPD_SCALE, C, world, rank + s * world)
+            ops.fill_synthetic_(planes.row(s, p), seed, p, UPD_SCALE, C, world, rank + s * world)
         ops.fill_synthetic_(w[s, :C], seed, W_PEER, W_SCALE, C, world, rank + s * world)
     w_full = torch.empty(n * world, dtype=torch.float32, device=dev) if world > 1 else None
-    tables = [ops.pointer_table([slab[p, s, :C] for p in range(K)], dev) for s in range(S)]
+    tables = planes.tables
     torch.cuda.synchronize()
     comp = torch.cuda.current_stream(dev)
     comm = torch.cuda.Stream(dev)
@@ -302,8 +305,11 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
             bad = [g for g in range(world)
                    if not bits_equal((w_full[g * C:g * C + m] if world > 1 else w[0, :m]).cpu().numpy(),
                                      oracle_expect(rule, K, m, seed, C, world, g))]
-            log(f"[rank 0] {name}: spot check vs oracle ({m} coords x {world} rank chunk(s)): "
-                f"{'bit-exact' if not bad else f'MISMATCH on ranks {bad}'}")
+            if S > 1 and not bits_equal(w[S - 1, :m].cpu().numpy(),  # rank 0's last plane too
+                                        oracle_expect(rule, K, m, seed, C, world, (S - 1) * world)):
+                bad.append(f"rank 0 plane {S - 1}")
+            log(f"[rank 0] {name}: spot check vs oracle ({m} coords x {world} rank chunk(s)"
+                f"{' + the last plane' if S > 1 else ''}): {'bit-exact' if not bad else f'MISMATCH on {bad}'}")
             if bad:
                 raise SystemExit(f"bench: {name} output differs from the oracle")
         if world > 1:
@@ -337,14 +343,15 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
     if rule == "fedavg" and world == 1 and not args.no_reference_gpu:
         # the reference's aggregation loop (aggregator/aggregation.py:15-38) as a
         # node on this GPU runs it: torch ops over the same resident updates
-        ws = w[0, :C]
-
+        # (coordinate-wise, so chunk by chunk is the same computation)
         def reference_step():
-            acc = torch.zeros_like(ws)  # :15
-            for p in range(K):  # :25-28
-                acc += slab[p, 0, :C]
-            acc /= K  # :31-32
-            ws.add_(0.1 * acc)  # :36-38 (`+=` on the state_dict tensor)
+            for s in range(S):
+                ws = w[s, :C]
+                acc = torch.zeros_like(ws)  # :15
+                for p in range(K):  # :25-28
+                    acc += planes.row(s, p)
+                acc /= K  # :31-32
+                ws.add_(0.1 * acc)  # :36-38 (`+=` on the state_dict tensor)
 
         reference_step()
         torch.cuda.synchronize()
@@ -353,7 +360,7 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
             reference_step()
         torch.cuda.synchronize()
         ref_s = (time.perf_counter() - t0) / 2
-    del slab, w, w_full, tables
+    del planes, w, w_full, tables
     torch.cuda.empty_cache()
     step_s = elapsed / steps
     cpu = None
@@ -382,6 +389,7 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
                                + (" (cfg3 per-GPU tile; N=8 -> the 1B-coordinate job)" if name == "cfg3" else ""),
                    "rule": rule, "peers": K, "coords_per_gpu": n, "coords_total": n * world,
                    "parallelism": parallelism(c),
+                   "layout": f"{S} chunk-major plane(s) of {K} x {C:,} (sharded.PeerPlanes), one launch per plane",
                    "pct_hbm_peak_step": round(4 * n * (K + 2) / step_s / 1e9 / HBM_PEAK_GBS, 4)}
                   | ({"per_rank": per_rank, "chunks_per_rank": S, "chunk_coords": C} | dist_info() if per_rank else {})
                   | ({"reference_on_gpu_ms_per_step": round(ref_s * 1e3, 3),
@@ -412,9 +420,9 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
     if nchunks % (world * chunks):
         raise SystemExit(f"cfg3-full: {nchunks} chunks do not split into tiles of {chunks} over {world} GPUs")
     per = nchunks // (world * chunks)  # tiles per rank
-    slab, w = pitched_slab(K, chunks, C, dev), pitched_slab(1, chunks, C, dev)[0]
+    planes, w = sharded.PeerPlanes(K, chunks, C, dev), pitched_slab(1, chunks, C, dev)[0]
     w_full = torch.empty(CFG3_COORDS, dtype=torch.float32, device=dev) if world > 1 else None
-    tables = [ops.pointer_table([slab[p, s, :C] for p in range(K)], dev) for s in range(chunks)]
+    tables = planes.tables
     comp = torch.cuda.current_stream(dev)
     comm = torch.cuda.Stream(dev)
     wall, kern, gath = [], [], []
@@ -427,7 +435,7 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
             vr = rank + u * chunks * world
             for s in range(chunks):
                 for p in range(K):
-                    ops.fill_synthetic_(slab[p, s, :C], seed, p, UPD_SCALE, C, world, vr + s * world)
+                    ops.fill_synthetic_(planes.row(s, p), seed, p, UPD_SCALE, C, world, vr + s * world)
                 ops.fill_synthetic_(w[s, :C], seed, W_PEER, W_SCALE, C, world, vr + s * world)
             torch.cuda.synchronize()
             if world > 1:
@@ -478,7 +486,7 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
         per_rank = [{"rank": int(r[0]), "ms_per_job": round(r[1], 3), "kernel_ms_sum": round(r[2], 3),
                      "allgather_ms_sum": round(r[3], 3)} for r in rows]
         tot, k_ms, g_ms = (max(r[i] for r in rows) for i in (1, 2, 3))
-    del slab, w, w_full, tables
+    del planes, w, w_full, tables
     torch.cuda.empty_cache()
     peer_bytes = K * CFG3_COORDS * 4
     return {

@@ -130,6 +130,53 @@ __device__ __forceinline__ void fedavg_elem(const float* const* __restrict__ pee
   if (w) stg(w + i, apply_lr(ldg(w + i), lr, m));
 }
 
+// Element-wise over E coordinates per lane at once -- first + stride * j, j
+// < E, those below n -- for views that are only 4-B aligned: every load
+// instruction still reads one contiguous 256 B per wave, and the lane keeps
+// E x 4 loads in flight where one coordinate at a time kept 8 (K = 256 over
+// 1.8M coordinates of 8-B aligned rows: 0.18 of HBM peak that way,
+// tools/grid_ab.py).  Each coordinate sums its peers in list order from +0.
+template <int E, bool RECIP>
+__device__ __forceinline__ void fedavg_scalar(const float* const* __restrict__ peers, int K, int64_t n,
+                                              int64_t first, int stride, float* w, float* out, float lr) {
+  constexpr int U = 4;
+  bool ok[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) ok[j] = first + static_cast<int64_t>(stride) * j < n;
+  float acc[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) acc[j] = 0.f;  // +0 init (:15)
+  int k = 0;
+  for (; k + U <= K; k += U) {
+    float x[U][E];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float* p = table_at(peers, k + u) + first;
+#pragma unroll
+      for (int j = 0; j < E; ++j) x[u][j] = ok[j] ? ldg_nt(p + static_cast<int64_t>(stride) * j) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)  // strictly in list order (:25-28)
+#pragma unroll
+      for (int j = 0; j < E; ++j) acc[j] += x[u][j];
+  }
+  for (; k < K; ++k) {
+    const float* p = table_at(peers, k) + first;
+#pragma unroll
+    for (int j = 0; j < E; ++j) acc[j] += ok[j] ? ldg_nt(p + static_cast<int64_t>(stride) * j) : 0.f;
+  }
+  const float fk = static_cast<float>(K);
+  const float inv = RECIP ? 1.0f / fk : 0.f;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    if (!ok[j]) continue;
+    const int64_t i = first + static_cast<int64_t>(stride) * j;
+    const float m = div1<RECIP>(acc[j], fk, inv);  // (:31-32)
+    if (out) stg(out + i, m);
+    if (w) stg(w + i, apply_lr(ldg(w + i), lr, m));  // (:36-38)
+  }
+}
+
 template <int NV, bool RECIP>
 __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ peers, int K,
                                             int64_t n, int64_t tile0, float* w, float* out,
@@ -151,13 +198,7 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
     }
     return;
   }
-#pragma unroll 1
-  for (int v = 0; v < NV; ++v)
-#pragma unroll 1
-    for (int e = 0; e < 4; ++e) {
-      const int64_t i = base + kBlock * 4 * v + e;
-      if (i < n) fedavg_elem<RECIP>(peers, K, i, w, out, lr);
-    }
+  fedavg_scalar<4 * NV, RECIP>(peers, K, n, tile0 + threadIdx.x, kBlock, w, out, lr);
 }
 
 // Flat buffer, one tile per block, tiles tile_base, tile_base + 1, ...  K
@@ -206,7 +247,6 @@ constexpr int kSPer = kSTile / 256 / kSL;    // DMA instructions per loader per 
 constexpr int kSRpw = kSTile / 256 / kSC;    // ds_read_b128 per consumer lane per stage
 static_assert((kSS - 2) * kSPer <= 63, "vmcnt is 6 bits");
 static_assert(kSRpw == 4, "lds_read4");
-constexpr int kSRoundsPerBlockMax = 8;       // grid <= 8 blocks per CU (one resident at a time)
 constexpr int kSplitMinK = 16;
 
 #define P2P_LDS __attribute__((address_space(3)))
@@ -264,9 +304,9 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
   const int wv = __builtin_amdgcn_readfirstlane(tid_x() >> 6), lane = tid_x() & 63;
   if (!SEGS && !all_aligned16(peers, K, w, out)) {
     // 4-B-aligned views: element-wise, same op order, no LDS (block-uniform)
-    for (int64_t t = b; t < ntiles; t += G)
-      for (int e = tid_x(); e < kSTile; e += 64 * (kSL + kSC))
-        fedavg_elem<RECIP>(peers, K, t * kSTile + e, w, out, lr);
+    constexpr int kT = 64 * (kSL + kSC);
+    for (int64_t t = b; t < ntiles; t += G)  // 11 x 768 >= 8192: the tile's end bounds the last
+      fedavg_scalar<(kSTile + kT - 1) / kT, RECIP>(peers, K, (t + 1) * kSTile, t * kSTile + tid_x(), kT, w, out, lr);
     return;
   }
   const int64_t N = (ntiles - b + G - 1) / G * K;  // stages (= barriers) of this block
@@ -377,9 +417,8 @@ static int device_cus() {
 // every CU gets the same number of 32-KiB x K tiles -- and the VGPR kernel
 // the rest (fewer than one tile per CU, plus the ragged tail), in 4096-float
 // tiles that many blocks share per CU: 1907 tiles (a cfg3 chunk at 8 GPUs) as
-// 8 split rounds would leave half the CUs idle in the last one.  The grid is
-// CUs x R blocks with R the largest divisor of the round count <= 8 (equal
-// tiles per block).  K is the kernarg or, for the device-K path, k_max.
+// 8 split rounds would leave half the CUs idle in the last one.  K is the
+// kernarg or, for the device-K path, k_max.
 // Split tiles for `full` whole tiles: whole rounds of the CU count (0 below
 // one round or for K < kSplitMinK).
 static int64_t split_tiles_for(int K, int64_t full) {
@@ -387,16 +426,13 @@ static int64_t split_tiles_for(int K, int64_t full) {
   const int64_t cus = device_cus();
   return full / cus * cus;
 }
-// CUs x R blocks, R the largest divisor of the round count <= 8 (a tile
-// count that is not whole rounds -- a caller's own list -- still runs, one
-// block per tile up to that grid).
-static dim3 split_grid(int64_t tiles) {
-  const int64_t cus = device_cus(), rounds = tiles / cus;
-  if (rounds < 1) return dim3(static_cast<unsigned>(tiles));
-  int64_t r = kSRoundsPerBlockMax < rounds ? kSRoundsPerBlockMax : rounds;
-  while (r > 1 && rounds % r) --r;
-  return dim3(static_cast<unsigned>(cus * r));
-}
+// One block per tile: one block is resident per CU (128 KiB of LDS), so the
+// dispatcher hands each CU its next tile as it frees -- no block owns a
+// fixed share of a launch, which a prime round count made one block per CU
+// (59 rounds for a cfg3 tile).  Same-box A/B (tools/grid_ab.py,
+// profiles/r05/grid): never slower than CUs x R blocks of equal tiles, +0.6%
+// at 256 x 125M, +2.3% at 16 x 100M.
+static dim3 split_grid(int64_t tiles) { return dim3(static_cast<unsigned>(tiles)); }
 
 static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,
                         float lr, hipStream_t stream, bool recip = false) {

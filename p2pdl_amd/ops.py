@@ -62,9 +62,22 @@ def _check_f32(t: torch.Tensor, name: str, device) -> None:
 
 def pointer_table(tensors: Sequence[torch.Tensor], device) -> torch.Tensor:
     """Device int64 tensor of data pointers (one small non-blocking H2D copy
-    through the pinned staging ring)."""
+    through the pinned staging ring).  It remembers the shortest tensor it
+    points into, so a call over more elements than that raises instead of
+    reading past a peer buffer (``table_covers``)."""
     host = np.array([t.data_ptr() for t in tensors], dtype=np.int64)
-    return _RING.to_device(host, device).view(torch.int64)
+    table = _RING.to_device(host, device).view(torch.int64)
+    table._p2p_min_numel = min((t.numel() for t in tensors), default=0)
+    return table
+
+
+def table_covers(table: torch.Tensor, n: int, what: str = "table") -> None:
+    """A prebuilt pointer table must point into buffers of >= n elements
+    (checked when pointer_table built it; a table from elsewhere is the
+    caller's contract)."""
+    m = getattr(table, "_p2p_min_numel", None)
+    if m is not None and n > m:
+        raise ValueError(f"{what} points into buffers of {m} elements; the call covers {n}")
 
 
 def _peer_inputs(peers: Sequence[torch.Tensor], n: int, device):
@@ -98,6 +111,8 @@ def aggregate(peers: Sequence[torch.Tensor], rule="fedavg", *, w: torch.Tensor |
     k = len(peers) if table is None else table.numel()
     if table is None:
         table = _peer_inputs(peers, n, ref.device)
+    else:
+        table_covers(table, n)
     if r not in FEDAVG_RULES and k > MAX_ROBUST_PEERS:
         raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {k}")
     b = 0
@@ -674,6 +689,7 @@ def fedavg_apply_devk_(w: torch.Tensor, table: torch.Tensor, k_dev: torch.Tensor
     if not 1 <= k_max:
         raise ValueError(f"k_max must be >= 1, got {k_max}")
     _check_tensor(table, "table", (torch.int64, torch.uint64), None, dev, min_numel=k_max)
+    table_covers(table, w.numel())
     _check_tensor(k_dev, "k_dev", torch.int32, None, dev, min_numel=1)
     with torch.cuda.device(w.device):
         N.check(N.lib().p2p_fedavg_apply_devk_f32(table.data_ptr(), k_dev.data_ptr(), k_max, w.numel(),

@@ -19,8 +19,9 @@ Two data layouts use the same plan:
   * replicated inputs (a tester holding every full update): ``sharded_aggregate_``
     reads each rank's owned ranges in place from the full buffers;
   * memory-sharded inputs (cfg3: 1.02 TB of updates never fit one GPU): each
-    rank holds only its owned coordinates (``ChunkPlan.local_len``), as in
-    bench.py, and gathers into the global model.
+    rank holds only its owned coordinates (``ChunkPlan.local_len``) in
+    ``PeerPlanes`` -- chunk-major, one plane of K peer rows per chunk -- and
+    gathers into the global model (bench.py).
 """
 from __future__ import annotations
 
@@ -31,6 +32,54 @@ import torch
 import torch.distributed as dist
 
 DEFAULT_CHUNK = 16 * 1024 * 1024  # coordinates per chunk (64 MB of fp32)
+
+# A plane's K peer rows span at most this much address space.  The streaming
+# kernels read a K-row plane faster when it is compact: same box, interleaved
+# (tools/grid_ab.py layout, profiles/r05/layout), 256 peers x 100M
+# coordinates as 8 planes of 12.8 GB against one row-major 102 GB slab:
+# FedAvg 0.844 vs 0.814 of HBM peak, median 0.827 vs 0.780, trimmed mean
+# equal (VALU-bound); 256 x 15.6M rows at a 62.5 MB pitch (16 GB) 0.83-0.85
+# against 0.78-0.80 at a 500 MB pitch (128 GB).  Same bytes, same kernels.
+PLANE_BYTES = 16 << 30
+ROW_ALIGN = 64  # fp32 elements: every peer row of a plane starts a 256-B boundary
+
+
+def plane_count(k: int, n: int, at_least: int = 1) -> int:
+    """Chunks S >= at_least that split n coordinates evenly (n % S == 0) into
+    planes of k rows spanning <= PLANE_BYTES each (the first such S; n itself
+    when nothing smaller divides it)."""
+    s = max(at_least, -(-(k * n * 4) // PLANE_BYTES), 1)
+    while n % s:
+        s += 1
+    return s
+
+
+class PeerPlanes:
+    """The memory-sharded receive layout of one rank: S chunks of C
+    coordinates from each of K peers, CHUNK-MAJOR -- plane s holds chunk s of
+    every peer as K rows of C' = C rounded up to ROW_ALIGN floats, so one
+    launch over chunk s reads one compact K x C' region (PLANE_BYTES).
+    ``row(s, p)`` is peer p's chunk s (a 256-B aligned view to land into),
+    ``tables[s]`` the device pointer table of plane s, ``reduce_(s, w, ...)``
+    the rule over it (the HIP kernels; no fallback)."""
+
+    def __init__(self, k: int, chunks: int, chunk: int, device):
+        from . import ops
+
+        self.k, self.chunks, self.chunk = int(k), int(chunks), int(chunk)
+        self.pitch = -(-self.chunk // ROW_ALIGN) * ROW_ALIGN
+        self.data = torch.empty((self.chunks, self.k, self.pitch), dtype=torch.float32, device=device)
+        self.tables = [ops.pointer_table([self.row(s, p) for p in range(self.k)], device)
+                       for s in range(self.chunks)]
+
+    def row(self, s: int, p: int) -> torch.Tensor:
+        return self.data[s, p, :self.chunk]
+
+    def reduce_(self, s: int, w: torch.Tensor, rule="fedavg", *, lr: float = 0.1,
+                trim_frac: float = 0.2) -> None:
+        from . import ops
+
+        ops.aggregate(None, rule, w=w, lr=lr, trim_frac=trim_frac, table=self.tables[s])
 
 
 @dataclass(frozen=True)

@@ -131,17 +131,21 @@ def test_fedavg_vs_oracle(cuda, k, n):
     assert_bits_equal(host(wt), w_ref, what="apply")
 
 
-def test_fedavg_unaligned_views(cuda):
-    """Peers that are 4-B but not 16-B aligned take the scalar path, same bits."""
-    n, k = 5000, 5
-    raw = [oracle.synth(n + 3, 77, p, 1e-2) for p in range(k)]
-    w = oracle.synth(n, 77, 0xFFFFF, 5e-2)
+@pytest.mark.parametrize("k,n", [(5, 5000), (1, 1), (3, 4095), (4, 4097), (8, 100_003), (17, 8192 * 300 + 7),
+                                 (256, 70_001)])
+def test_fedavg_unaligned_views(cuda, k, n):
+    """Peers that are 4-B but not 16-B aligned take the scalar path
+    (fedavg_scalar: many coordinates per lane, peers unrolled by 4 -- K not a
+    multiple of 4, ragged n), same bits, mean and apply."""
+    raw = [oracle.synth(n + 3, 77 + k, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, 77 + k, 0xFFFFF, 5e-2)
     dev_raw = [to_dev(r, cuda) for r in raw]
     views = [d[1 + (p % 3):1 + (p % 3) + n] for p, d in enumerate(dev_raw)]
-    w_ref, _ = oracle.fedavg([r[1 + (p % 3):1 + (p % 3) + n] for p, r in enumerate(raw)], w)
-    wt = to_dev(w, cuda)
-    ops.fedavg_apply_(wt, views)
-    assert_bits_equal(host(wt), w_ref, what="unaligned")
+    w_ref, out_ref = oracle.fedavg([r[1 + (p % 3):1 + (p % 3) + n] for p, r in enumerate(raw)], w, want_out=True)
+    wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate(views, "fedavg", w=wt, out=out)
+    assert_bits_equal(host(out), out_ref, what="unaligned mean")
+    assert_bits_equal(host(wt), w_ref, what="unaligned apply")
 
 
 def test_fedavg_large_k64_resnet_shape(cuda):
@@ -227,6 +231,19 @@ def test_fedavg_split_kernel_unaligned_rows_and_mean_only(cuda):
     got = host(ops.mean(rows))
     for a, b in split_windows(n):
         assert_bits_equal(got[a:b], split_expect(k, seed, a, b)[1], what=f"mean only [{a}, {b})")
+
+
+def test_prebuilt_table_shorter_than_the_call_raises(cuda):
+    """A pointer table over views shorter than w is refused on the host (a
+    kernel would read past the peers' buffers)."""
+    rows = [torch.zeros(1000, dtype=torch.float32, device=cuda) for _ in range(4)]
+    table = ops.pointer_table(rows, cuda)
+    w = torch.zeros(1001, dtype=torch.float32, device=cuda)
+    with pytest.raises(ValueError, match="1000 elements"):
+        ops.aggregate(None, "fedavg", w=w, table=table)
+    with pytest.raises(ValueError, match="1000 elements"):
+        ops.fedavg_apply_devk_(w, table, torch.tensor([4], dtype=torch.int32, device=cuda), 4)
+    ops.aggregate(None, "fedavg", w=w[:1000], table=table)  # covered: runs
 
 
 def test_fedavg_split_kernel_devk(cuda):

@@ -15,6 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
+from p2pdl_amd import sharded
 from p2pdl_amd.sharded import ChunkPlan, sharded_aggregate_
 
 
@@ -27,6 +28,47 @@ def test_chunk_plan_covers_every_coordinate_once():
                 seen[st:st + ln] += 1
             assert plan.local_len(r) == sum(ln for _, ln in plan.owned(r))
         assert (seen == 1).all(), (n, world, chunk)
+
+
+@pytest.mark.parametrize("k,n,at_least,want", [
+    (256, 125_000_000, 1, 8),    # cfg3 tile: 128 GB -> 8 planes of 16 GB
+    (256, 125_000_000, 8, 8),    # N > 1: the all-gather chunks already fit
+    (256, 100_000_000, 1, 8),    # 102 GB: 7 would do, 8 divides 100M
+    (128, 100_000_000, 1, 4),    # cfg4: 51 GB
+    (64, 11_689_512, 1, 1),      # cfg2: 3 GB, one plane
+    (256, 7, 1, 1),
+    (4, 13, 2, 13),              # nothing between 2 and 13 divides a prime
+])
+def test_plane_count(k, n, at_least, want):
+    s = sharded.plane_count(k, n, at_least)
+    assert s == want and n % s == 0
+    assert s == 1 or k * (n // s) * 4 <= sharded.PLANE_BYTES or s == n
+
+
+@pytest.mark.gpu
+def test_peer_planes_layout_and_reduce(cuda):
+    """PeerPlanes: chunk-major planes, 256-B aligned rows, one table per
+    plane; reduce_ over each plane equals one flat reduction of the peers'
+    concatenated chunks (bit-exact against the oracle)."""
+    from p2pdl_amd import ops
+
+    k, chunks, chunk, seed = 20, 3, 70_001, 0x91A
+    planes = sharded.PeerPlanes(k, chunks, chunk, cuda)
+    assert planes.data.shape == (chunks, k, 70_016) and planes.pitch % 64 == 0
+    assert all(planes.row(s, p).data_ptr() % 256 == 0 for s in range(chunks) for p in range(k))
+    assert planes.row(1, 0).data_ptr() - planes.row(0, k - 1).data_ptr() == planes.pitch * 4  # plane-major
+    peers = [oracle.synth(chunks * chunk, seed, p, 1e-2) for p in range(k)]
+    w = oracle.synth(chunks * chunk, seed, 0xFFFFF, 5e-2)
+    for s in range(chunks):
+        for p in range(k):
+            planes.row(s, p).copy_(torch.from_numpy(peers[p][s * chunk:(s + 1) * chunk]))
+    wt = torch.from_numpy(w.copy()).to(cuda)
+    for s in range(chunks):
+        planes.reduce_(s, wt[s * chunk:(s + 1) * chunk], "fedavg")
+    w_ref, _ = oracle.fedavg(peers, w)
+    assert np.array_equal(wt.cpu().numpy().view(np.uint32), w_ref.view(np.uint32))
+    with pytest.raises(ValueError):  # a w longer than the plane's rows
+        planes.reduce_(0, torch.zeros(chunk + 1, device=cuda))
 
 
 def test_global_index_matches_device_prng_mapping():
