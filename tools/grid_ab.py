@@ -195,6 +195,51 @@ def layout_ab(K, n, S, reps, dev, rules=("fedavg", "median", "trimmed")):
     torch.cuda.empty_cache()
 
 
+def planes_onelaunch(K, n, S, reps, dev, rules=("fedavg", "median", "trimmed")):
+    """Chunk-major planes: S launches (one per plane) against ONE segment-table
+    launch over all planes (ops.aggregate_segments_), interleaved, bit-compared."""
+    from p2pdl_amd import sharded
+
+    C = n // S
+    pl = sharded.PeerPlanes(K, S, C, dev)
+    for s_ in range(S):
+        for p in range(K):
+            ops.fill_synthetic_(pl.row(s_, p), 0x5EED0002, p, 1e-2, C, 1, s_)
+    w0 = torch.empty((S, C), dtype=torch.float32, device=dev)
+    for s_ in range(S):
+        ops.fill_synthetic_(w0[s_], 0x5EED0002, 0xFFFFF, 5e-2, C, 1, s_)
+    peer_lists = [[pl.row(s_, p) for s_ in range(S)] for p in range(K)]
+    for rule in rules:
+        fns = {f"{S} launches": lambda w: [pl.reduce_(s_, w[s_], rule) for s_ in range(S)],
+               "one segment launch": lambda w: ops.aggregate_segments_([w[s_] for s_ in range(S)], peer_lists, rule)}
+        got = []
+        for fn in fns.values():
+            x = w0.clone()
+            fn(x)
+            torch.cuda.synchronize()
+            got.append(x.cpu().numpy().view(np.uint32))
+        same = np.array_equal(got[0], got[1])
+        ms = {k: [] for k in fns}
+        w = w0.clone()
+        for _ in range(reps):
+            for name, fn in fns.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda._sleep(1_000_000)
+                e0.record()
+                fn(w)
+                e1.record()
+                torch.cuda.synchronize()
+                ms[name].append(e0.elapsed_time(e1))
+        alg = 4.0 * n * (K + 2)
+        print(f"{rule} K={K} n={n:,} planes {S}: bit-identical {same}")
+        for name, v in ms.items():
+            v = sorted(v)
+            t = v[len(v) // 2]
+            print(f"  {name:24s} median {t:.4f} ms  {alg / t / 1e6 / 8000:.4f} of 8 TB/s  best {v[0]:.4f}", flush=True)
+    del pl
+    torch.cuda.empty_cache()
+
+
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     mode = sys.argv[2] if len(sys.argv) > 2 else "chunks"
@@ -221,6 +266,9 @@ def main():
     elif mode == "layout":
         layout_ab(256, 100_000_000, 8, reps, dev)
         layout_ab(128, 100_000_000, 4, reps, dev, rules=("median", "trimmed", "fedavg"))
+    elif mode == "onelaunch":
+        planes_onelaunch(128, 100_000_000, 4, reps, dev)
+        planes_onelaunch(256, 100_000_000, 8, reps, dev)
     elif mode == "vgpr":
         vgpr_views(reps, dev)
     elif mode == "pitch":
