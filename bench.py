@@ -268,30 +268,25 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
 
     gath = []
 
+    wviews = [w[s, :C] for s in range(S)]
+
     def step(record=False):
-        for s in range(S):
-            ws = w[s, :C]
-            if record:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(comp)
-            ops.aggregate(None, rule, w=ws, lr=0.1, table=tables[s])
-            if record:
-                e1.record(comp)
-                kern.append((e0, e1))
-            if world > 1:
-                done = torch.cuda.Event()
-                done.record(comp)
-                comm.wait_event(done)
-                with torch.cuda.stream(comm):
-                    if record:
-                        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        g0.record(comm)
-                    dist.all_gather_into_tensor(w_full[s * C * world:(s + 1) * C * world], ws)
-                    if record:
-                        g1.record(comm)
-                        gath.append((g0, g1))
-        if world > 1:
-            comp.wait_stream(comm)
+        # the product's round (sharded.PeerPlanes.aggregate_gather_): every
+        # plane reduced on the compute stream, its all-gather beside the next
+        ev = {}
+
+        def hook(s, phase, stream):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            ev[(s, phase)] = e
+
+        planes.aggregate_gather_(wviews, w_full, rule=rule, lr=0.1, comm=comm if world > 1 else None,
+                                 hook=hook if record else None)
+        if record:
+            for s in range(S):
+                kern.append((ev[(s, "reduce0")], ev[(s, "reduce1")]))
+                if world > 1:
+                    gath.append((ev[(s, "gather0")], ev[(s, "gather1")]))
 
     # correctness spot check of the first warmup step: rank 0 checks the first
     # m coordinates of EVERY rank's first chunk, in its own w and, at N > 1,
@@ -421,6 +416,7 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
         raise SystemExit(f"cfg3-full: {nchunks} chunks do not split into tiles of {chunks} over {world} GPUs")
     per = nchunks // (world * chunks)  # tiles per rank
     planes, w = sharded.PeerPlanes(K, chunks, C, dev), pitched_slab(1, chunks, C, dev)[0]
+    wviews = [w[s, :C] for s in range(chunks)]
     w_full = torch.empty(CFG3_COORDS, dtype=torch.float32, device=dev) if world > 1 else None
     tables = planes.tables
     comp = torch.cuda.current_stream(dev)
@@ -440,30 +436,26 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
-            ev = []
+            ev = {}
+
+            def hook(s, phase, stream):
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(stream)
+                ev[(s, phase)] = e
+
             start = torch.cuda.Event(enable_timing=True)
             start.record(comp)
-            for s in range(chunks):
-                e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-                e[0].record(comp)
-                ops.aggregate(None, "fedavg", w=w[s, :C], lr=0.1, table=tables[s])
-                e[1].record(comp)
-                if world > 1:
-                    comm.wait_event(e[1])
-                    g0 = ((u * chunks + s) * world) * C
-                    with torch.cuda.stream(comm):
-                        e[2].record(comm)
-                        dist.all_gather_into_tensor(w_full[g0:g0 + world * C], w[s, :C])
-                        e[3].record(comm)
-                ev.append(e)
-            comp.wait_stream(comm)
+            # tile u's chunks are global rounds u*chunks .. u*chunks+chunks-1
+            tile_full = w_full[u * chunks * world * C:(u + 1) * chunks * world * C] if world > 1 else None
+            planes.aggregate_gather_(wviews, tile_full, rule="fedavg", lr=0.1, comm=comm if world > 1 else None,
+                                     hook=hook)
             end = torch.cuda.Event(enable_timing=True)
             end.record(comp)
             torch.cuda.synchronize()
             w_tot += start.elapsed_time(end)
-            k_tot += sum(e[0].elapsed_time(e[1]) for e in ev)
+            k_tot += sum(ev[(s, "reduce0")].elapsed_time(ev[(s, "reduce1")]) for s in range(chunks))
             if world > 1:
-                g_tot += sum(e[2].elapsed_time(e[3]) for e in ev)
+                g_tot += sum(ev[(s, "gather0")].elapsed_time(ev[(s, "gather1")]) for s in range(chunks))
             if not checked and not args.no_check and rank == 0:
                 m = 4096
                 got = (w_full[:m] if world > 1 else w[0, :m]).cpu().numpy()  # global chunk 0: rank 0, tile 0

@@ -61,16 +61,24 @@ class PeerPlanes:
     launch over chunk s reads one compact K x C' region (PLANE_BYTES).
     ``row(s, p)`` is peer p's chunk s (a 256-B aligned view to land into),
     ``tables[s]`` the device pointer table of plane s, ``reduce_(s, w, ...)``
-    the rule over it (the HIP kernels; no fallback)."""
+    the rule over it (the HIP kernels; no fallback) and ``aggregate_gather_``
+    one whole round: every plane, each plane's all-gather beside the next
+    plane's reduction."""
 
     def __init__(self, k: int, chunks: int, chunk: int, device):
-        from . import ops
-
         self.k, self.chunks, self.chunk = int(k), int(chunks), int(chunk)
         self.pitch = -(-self.chunk // ROW_ALIGN) * ROW_ALIGN
         self.data = torch.empty((self.chunks, self.k, self.pitch), dtype=torch.float32, device=device)
-        self.tables = [ops.pointer_table([self.row(s, p) for p in range(self.k)], device)
-                       for s in range(self.chunks)]
+        self._tables = None
+
+    @property
+    def tables(self):
+        if self._tables is None:  # device pointer tables (the HIP path only)
+            from . import ops
+
+            self._tables = [ops.pointer_table([self.row(s, p) for p in range(self.k)], self.data.device)
+                            for s in range(self.chunks)]
+        return self._tables
 
     def row(self, s: int, p: int) -> torch.Tensor:
         return self.data[s, p, :self.chunk]
@@ -80,6 +88,58 @@ class PeerPlanes:
         from . import ops
 
         ops.aggregate(None, rule, w=w, lr=lr, trim_frac=trim_frac, table=self.tables[s])
+
+    def aggregate_gather_(self, ws: Sequence[torch.Tensor], w_full: torch.Tensor | None = None, *,
+                          rule="fedavg", lr: float = 0.1, trim_frac: float = 0.2, group=None,
+                          comm=None, reduce: Callable | None = None, hook: Callable | None = None) -> None:
+        """One aggregation round over every plane.  ``ws[s]`` is this rank's
+        chunk s of w -- global chunk s*G + rank (ChunkPlan's round robin) --
+        updated in place.  With ``w_full`` and an initialised process group,
+        round s's all-gather writes every rank's chunk s to the contiguous
+        w_full[s*G*C, (s+1)*G*C): on ``comm`` (a second stream) beside plane
+        s+1's reduction, the compute stream waiting for the last one; without
+        ``comm``, in line.  ``hook(s, phase, stream)`` runs at "reduce0" /
+        "reduce1" / "gather0" / "gather1" on the stream of that step (timing
+        events); ``reduce(planes, s, w, rule, lr, trim_frac)`` replaces the HIP
+        reduction (the CPU gloo tests)."""
+        if len(ws) != self.chunks:
+            raise ValueError(f"{len(ws)} w chunks for {self.chunks} planes")
+        gather = w_full is not None and dist.is_initialized()
+        G = dist.get_world_size(group) if gather else 1
+        C = self.chunk
+        if gather and w_full.numel() < self.chunks * G * C:
+            raise ValueError(f"w_full has {w_full.numel()} elements, the round needs {self.chunks * G * C}")
+        comp = torch.cuda.current_stream(self.data.device) if self.data.is_cuda else None
+        for s in range(self.chunks):
+            if hook:
+                hook(s, "reduce0", comp)
+            if reduce is None:
+                self.reduce_(s, ws[s], rule, lr=lr, trim_frac=trim_frac)
+            else:
+                reduce(self, s, ws[s], rule, lr, trim_frac)
+            if hook:
+                hook(s, "reduce1", comp)
+            if not gather:
+                continue
+            out = w_full[s * G * C:(s + 1) * G * C]
+            if comm is not None:
+                ev = torch.cuda.Event()
+                ev.record(comp)
+                comm.wait_event(ev)
+                with torch.cuda.stream(comm):
+                    if hook:
+                        hook(s, "gather0", comm)
+                    dist.all_gather_into_tensor(out, ws[s], group=group)
+                    if hook:
+                        hook(s, "gather1", comm)
+            else:
+                if hook:
+                    hook(s, "gather0", comp)
+                dist.all_gather_into_tensor(out, ws[s].contiguous().clone(), group=group)
+                if hook:
+                    hook(s, "gather1", comp)
+        if gather and comm is not None:
+            comp.wait_stream(comm)
 
 
 @dataclass(frozen=True)

@@ -137,6 +137,64 @@ def test_gloo_world_byte_identical_to_single(world, rule, n, k, chunk):
     assert all(got[r] == want.tobytes() for r in range(world))
 
 
+def _planes_worker(rank, world, port, n, k, rule, S, q):
+    """Memory-sharded inputs: this rank holds only its owned chunks of every
+    peer, in PeerPlanes (CPU tensors here; the oracle reduces), and one
+    aggregate_gather_ reassembles the global model."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        C = n // (world * S)
+        plan = ChunkPlan(n, world, C)
+        owned = plan.owned(rank)
+        assert len(owned) == S and plan.tail == 0
+        peers = [oracle.synth(n, 29, p, 1e-2) for p in range(k)]
+        w = oracle.synth(n, 29, 0xFFFFF, 5e-2)
+        planes = sharded.PeerPlanes(k, S, C, "cpu")
+        for s, (st, ln) in enumerate(owned):
+            for p in range(k):
+                planes.row(s, p).copy_(torch.from_numpy(peers[p][st:st + ln]))
+        ws = [torch.from_numpy(w[st:st + ln].copy()) for st, ln in owned]
+        w_full = torch.zeros(n, dtype=torch.float32)
+
+        def reduce(pl, s, wchunk, rule_, lr, trim_frac):
+            oracle_reduce([pl.row(s, p) for p in range(pl.k)], wchunk, rule_, lr, trim_frac)
+
+        seen = []
+        planes.aggregate_gather_(ws, w_full, rule=rule, reduce=reduce, hook=lambda s, ph, st: seen.append((s, ph)))
+        assert seen == [(s, ph) for s in range(S) for ph in ("reduce0", "reduce1", "gather0", "gather1")]
+        q.put((rank, w_full.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,rule,n,k,S", [(2, "fedavg", 2 * 3 * 1001, 5, 3), (2, "trimmed", 2 * 2 * 640, 10, 2)])
+def test_gloo_peer_planes_round_byte_identical_to_single(world, rule, n, k, S):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_planes_worker, args=(r, world, port, n, k, rule, S, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    peers = [oracle.synth(n, 29, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, 29, 0xFFFFF, 5e-2)
+    if rule == "fedavg":
+        want, _ = oracle.fedavg(peers, w)
+    else:
+        want, _ = oracle.robust(peers, 2, oracle.trim_count(k), w=w)
+    assert all(got[r] == want.tobytes() for r in range(world))
+
+
+def test_peer_planes_checks_round_shapes():
+    planes = sharded.PeerPlanes(3, 2, 10, "cpu")
+    with pytest.raises(ValueError, match="w chunks"):
+        planes.aggregate_gather_([torch.zeros(10)], reduce=lambda *a: None)
+
+
 # ---------------------------------------------------------------- GPU leg
 def _gpu_worker(rank, world, port, n, k, rule, chunk, overlap, q):
     """One rank: the HIP reduce (the default of sharded_aggregate_) on cuda:0,

@@ -29,7 +29,8 @@ B="bench.py --no-sub --no-cpu-baseline --no-reference-gpu --steps 2 --warmup 1"
 # kernel stats of the default bench (all sub-records), CPU baselines skipped
 [ -n "$NO_STATS" ] || run 600 "$OUT/stats_bench.log" rocprofv3 --kernel-trace --stats $F -d "$OUT/stats_bench" -o bench -- python3 -u bench.py --no-cpu-baseline
 
-# HBM traffic per launch: workload kernel coords peers [extra bench args]
+# HBM traffic per launch (one launch per chunk-major plane, sharded.PeerPlanes):
+# workload kernel coords-per-launch peers [extra bench args]
 while IFS=: read -r w k c p extra; do
   [ -z "$w" ] && continue
   [ -n "$ONLY" ] && [[ " $ONLY " != *" $w "* ]] && continue
@@ -38,13 +39,13 @@ while IFS=: read -r w k c p extra; do
   done
   python3 tools/pmc_traffic.py "$OUT/pmc_FETCH_SIZE_$w" "$OUT/pmc_WRITE_SIZE_$w" "$k" "$w" "$c" "$p" "$OUT/traffic_$w.json" > /dev/null || exit 1
 done <<'EOS'
-cfg3:fedavg_split_kernel+fedavg_flat_kernel:125000000:256:--workload cfg3
+cfg3:fedavg_split_kernel+fedavg_flat_kernel:15625000:256:--workload cfg3
 cfg3-chunk:fedavg_split_kernel+fedavg_flat_kernel:15625000:256:--job cfg3-full --steps 1
 cfg2-dropin:fedavg_segments_kernel:11689512:64:--workload cfg2-dropin
-cfg4-median:robust_flat_kernel:100000000:128:--workload cfg4-median
-cfg4-trimmed:robust_flat_kernel:100000000:128:--workload cfg4-trimmed
-median256:robust_median_pair_kernel:100000000:256:--workload median256
-trimmed256:robust_pair_kernel:100000000:256:--workload trimmed256
+cfg4-median:robust_flat_kernel:25000000:128:--workload cfg4-median
+cfg4-trimmed:robust_flat_kernel:25000000:128:--workload cfg4-trimmed
+median256:robust_median_pair_kernel:12500000:256:--workload median256
+trimmed256:robust_pair_kernel:12500000:256:--workload trimmed256
 delta:delta_flat_kernel:1000000000:1:--workload delta
 EOS
 

@@ -266,6 +266,11 @@ def main():
     elif mode == "layout":
         layout_ab(256, 100_000_000, 8, reps, dev)
         layout_ab(128, 100_000_000, 4, reps, dev, rules=("median", "trimmed", "fedavg"))
+    elif mode == "rounds":
+        for _ in range(3):
+            spread(256, 15_625_000, 15_625_064, reps, dev)   # 7 split rounds + 115 tiles + tail
+            spread(256, 14_680_064, 14_680_128, reps, dev)   # exactly 7 rounds of 256 x 8192
+            spread(256, 16_777_216, 16_777_280, reps, dev)   # exactly 8 rounds
     elif mode == "onelaunch":
         planes_onelaunch(128, 100_000_000, 4, reps, dev)
         planes_onelaunch(256, 100_000_000, 8, reps, dev)
