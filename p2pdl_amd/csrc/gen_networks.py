@@ -728,6 +728,9 @@ def emit_classic():
     return lines
 
 
+NAN_CONE_TAGS = ("sort64", "sort128")  # the pair kernels' sorts (robust_pair.hip)
+
+
 def emit_fused():
     lines = HEADER + [
         "// Lowered to one instruction per computed value: P2P_LO / P2P_HI (two inputs; P2P_HIS also gets the",
@@ -753,6 +756,25 @@ def emit_fused():
         def ref(n):
             return f"v[{n}]" if n < kp else f"n{n}"
 
+        # The pair kernels' float paths test for NaN on output rank 0 alone:
+        # every instruction in its cone is a min (checked here), and emitted
+        # as the NaN-propagating form (P2P_LON / P2P_LO3N: v_minimum3_f32 on
+        # floats, the plain min on keys), so a NaN anywhere among the inputs
+        # reaches v[0] -- one compare where a packed-FMA chain over the loads
+        # took ~N/4 instructions.  NaN-free inputs: the same bits.
+        nan_cone = set()
+        if tag in NAN_CONE_TAGS:
+            byid = {i: (op, a) for i, op, a in ins}
+            stack = [prog.out[0]]
+            while stack:
+                n = stack.pop()
+                if n < kp or n in nan_cone:
+                    continue
+                assert byid[n][0] in ("lo", "lo3"), (tag, "rank-0 cone holds a non-min", n, byid[n][0])
+                nan_cone.add(n)
+                stack.extend(x for x in byid[n][1] if x is not None)
+            lines.append(f"  // rank-0 cone: {len(nan_cone)} NaN-propagating mins")
+
         seen = set()
         for i, op, a in ins:
             # hook(v, blk) runs before the first instruction that reads input
@@ -762,7 +784,9 @@ def emit_fused():
                 lines.append(f"  hook(v, {blk});")
                 seen.add(blk)
             if op == "lo":
-                rhs = f"P2P_LO({ref(a[0])}, {ref(a[1])})"
+                rhs = f"P2P_LO{'N' if i in nan_cone else ''}({ref(a[0])}, {ref(a[1])})"
+            elif op == "lo3" and i in nan_cone:
+                rhs = f"P2P_LO3N({ref(a[0])}, {ref(a[1])}, {ref(a[2])})"
             elif op == "hi":
                 rhs = (f"P2P_HIS({ref(a[0])}, {ref(a[1])}, {ref(a[2])})" if a[2] is not None
                        else f"P2P_HI({ref(a[0])}, {ref(a[1])})")

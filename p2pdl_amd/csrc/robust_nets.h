@@ -53,6 +53,18 @@ __device__ __forceinline__ float maximum3(float a, float b, float c) {
   asm volatile("v_maximum3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
 }
+// v_minimum3_f32 likewise (IEEE 754-2019 minimum); not volatile: the
+// scheduler may move it like the min it stands for.
+__device__ __forceinline__ float minimum3_nv(float a, float b, float c) {
+  float d;
+  asm("v_minimum3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ float maximum3_nv(float a, float b, float c) {
+  float d;
+  asm("v_maximum3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
 // INF_SAFE: the test of a padded network's slots, whose +-inf pad rows meet
 // (inf - inf in the FMA chain would send every tile to the key path): two
 // v_maximum3 chains, two values per instruction.
@@ -199,6 +211,22 @@ template <bool ASC, typename T>
 __device__ __forceinline__ T lo3(T a, T b, T c) { return lo2<ASC>(lo2<ASC>(a, b), c); }
 template <bool ASC, typename T>
 __device__ __forceinline__ T hi3(T a, T b, T c) { return hi2<ASC>(hi2<ASC>(a, b), c); }
+// The NaN-propagating mins of a sort's rank-0 cone (gen_networks.py
+// NAN_CONE_TAGS): on floats v_minimum3_f32 (v_maximum3 descending) -- NaN in
+// any operand gives NaN, otherwise one of the operands bit for bit, -0 < +0,
+// exactly what v_min / v_min3 select on NaN-free floats; on keys the plain min.
+template <bool ASC, typename T>
+__device__ __forceinline__ T lon(T a, T b) { return lo2<ASC>(a, b); }
+template <bool ASC, typename T>
+__device__ __forceinline__ T lo3n(T a, T b, T c) { return lo3<ASC>(a, b, c); }
+template <bool ASC>
+__device__ __forceinline__ fk lon(fk a, fk b) { return fk{ASC ? minimum3_nv(a.x, b.x, b.x) : maximum3_nv(a.x, b.x, b.x)}; }
+template <bool ASC>
+__device__ __forceinline__ fx lon(fx a, fx b) { return fx{ASC ? minimum3_nv(a.x, b.x, b.x) : maximum3_nv(a.x, b.x, b.x)}; }
+template <bool ASC>
+__device__ __forceinline__ fk lo3n(fk a, fk b, fk c) { return fk{ASC ? minimum3_nv(a.x, b.x, c.x) : maximum3_nv(a.x, b.x, c.x)}; }
+template <bool ASC>
+__device__ __forceinline__ fx lo3n(fx a, fx b, fx c) { return fx{ASC ? minimum3_nv(a.x, b.x, c.x) : maximum3_nv(a.x, b.x, c.x)}; }
 __device__ __forceinline__ uint32_t med3(uint32_t a, uint32_t b, uint32_t c) { return umed3(a, b, c); }
 __device__ __forceinline__ kx med3(kx a, kx b, kx c) { return kx{umed3(a.k, b.k, c.k)}; }
 __device__ __forceinline__ fk med3(fk a, fk b, fk c) { return fk{__builtin_amdgcn_fmed3f(a.x, b.x, c.x)}; }
@@ -207,6 +235,8 @@ __device__ __forceinline__ fx med3(fx a, fx b, fx c) { return fx{__builtin_amdgc
 #define P2P_HI(a, b) hi2<ASC>((a), (b))
 #define P2P_HIS(a, b, lo) hi_sib<ASC>((a), (b), (lo))
 #define P2P_LO3(a, b, c) lo3<ASC>((a), (b), (c))
+#define P2P_LON(a, b) lon<ASC>((a), (b))
+#define P2P_LO3N(a, b, c) lo3n<ASC>((a), (b), (c))
 #define P2P_HI3(a, b, c) hi3<ASC>((a), (b), (c))
 #define P2P_MED3(a, b, c) med3((a), (b), (c))
 // the round-2 two-input form (gen_networks.py --classic, A/B builds)
@@ -221,6 +251,8 @@ __device__ __forceinline__ fx med3(fx a, fx b, fx c) { return fx{__builtin_amdgc
 #undef P2P_HI
 #undef P2P_HIS
 #undef P2P_LO3
+#undef P2P_LON
+#undef P2P_LO3N
 #undef P2P_HI3
 #undef P2P_MED3
 

@@ -130,12 +130,6 @@ struct Pads {
   int m = 2 * kHalf - 2 * 51;  // trimmed: kept ranks
 };
 
-// NaN test of N consecutive loaded keys (robust_nets.h nan_lanes).
-template <int N, bool INF_SAFE = false>
-__device__ __forceinline__ uint64_t list_nan_mask(const uint32_t* v) {
-  return nan_lanes<N, INF_SAFE>([&](int j) { return __uint_as_float(v[j]); });
-}
-
 // One half sorted in T's domain (the block's: keys if either half holds a
 // NaN); returns the aggregate, valid in wave 0.  Both waves pass the same
 // number of block barriers.
@@ -159,18 +153,18 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
                                              const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0,
                                              int K = 2 * kHalf, const Pads& pd = Pads{}, int pr = 0) {
   constexpr int Q = kHalf / 2;  // 64 keys per sorted list
-  // FLAGS: each list's NaN test right before its sort, so sorting p overlaps
-  // q's loads (a test of all 128 up front waited for every load: +3.5% time)
+  // FLAGS: the NaN test is one compare of each sort's rank-0 output: every
+  // min in its cone propagates NaN (gen_networks.py NAN_CONE_TAGS), so a NaN
+  // among a list's 64 keys reaches p[0] / q[0]
   T p[Q], q[Q];
-  uint64_t nan = 0;
-  if constexpr (FLAGS) nan = list_nan_mask<Q, PAD>(v);
 #pragma unroll
   for (int j = 0; j < Q; ++j) p[j] = from_bits<T>(v[j]);
   sort_full<Q>(p);
-  if constexpr (FLAGS) nan |= list_nan_mask<Q, PAD>(v + Q);
 #pragma unroll
   for (int j = 0; j < Q; ++j) q[j] = from_bits<T>(v[Q + j]);
   sort_full<Q>(q);
+  uint64_t nan = 0;
+  if constexpr (FLAGS) nan = unordered_mask(bits_f(p[0]), bits_f(q[0]));
   const bool has_nan = FLAGS && uniform(nan != 0);  // to a bool at once (a live mask spilled SGPRs)
   pin(p);
   pin(q);
@@ -219,16 +213,13 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   T x[kHalf];
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) x[j] = from_bits<T>(v[j]);
-  // FLAGS: the first half's NaN test before the sort, the second half's when
-  // the sort first reads it (NanHook at block 4), so the sort of the first 64
-  // overlaps the last loads
+  // FLAGS: the NaN test is one compare of the sort's rank-0 output, which
+  // every NaN among the 128 keys reaches (the NaN-propagating mins of its
+  // cone, gen_networks.py NAN_CONE_TAGS) -- where a packed-FMA chain over the
+  // loads took 34 instructions per wave
+  sort_full<kHalf>(x);
   uint64_t nan = 0;
-  if constexpr (FLAGS) {
-    nan = list_nan_mask<kHalf / 2, PAD>(v);
-    sort_full<kHalf>(x, NanHook<4, 4, PAD ? 0 : 1 << 20>{nan});
-  } else {
-    sort_full<kHalf>(x);
-  }
+  if constexpr (FLAGS) nan = unordered_mask(bits_f(x[0]), bits_f(x[0]));
   const bool has_nan = FLAGS && uniform(nan != 0);
   pin(x);
   // Batcher's odd-even merge of A (wave 0) and B (wave 1), split by parity:

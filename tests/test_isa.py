@@ -9,7 +9,10 @@ p2pdl_amd/libp2pdl_hip.so (llvm-objdump, tools/isa_stats.py) and assert
   * every function that runs the float network also issues the explicit NaN
     test over every key it loads (asm v_pk_fma_f32 chains, through which NaN
     propagates, ended by a v_cmp_u_f32; or one compare per two keys) -- the
-    compiler would fold an isnan() away under this flag, asm it cannot;
+    compiler would fold an isnan() away under this flag, asm it cannot; the
+    pair kernels instead compare their sorts' rank-0 outputs, whose cones are
+    asm v_minimum3_f32 throughout (gen_networks.py asserts the cone holds
+    only mins and reaches every input);
   * every key-path function (pair_keys, robust_coord_keys) and every MODE 0
     kernel sorts with integer min / max / med3 only, so a NaN key is ranked
     by its bits whatever the float mode;
@@ -82,7 +85,10 @@ def test_float_network_always_behind_the_nan_test(funcs):
         # counts the two extra keys its first instruction folds); the loads
         # include one that is not a key (the w read of the apply)
         loads = sum(v for k, v in c.items() if k.startswith("global_load") and "lds" not in k)
-        assert cmps > 0 and 4 * pk + 2 * mx + 2 * cmps >= loads - 1 > 0, (name, cmps, pk, mx, loads)
+        # the pair kernels' rank-0 cones: 76 NaN-propagating mins per sort128,
+        # 36 per sort64 (two per median wave)
+        rank0 = c["v_minimum3_f32"] >= 72
+        assert cmps > 0 and (rank0 or 4 * pk + 2 * mx + 2 * cmps >= loads - 1 > 0), (name, cmps, pk, mx, loads)
         checked += 1
     assert checked >= 6
 
