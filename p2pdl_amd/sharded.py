@@ -46,12 +46,13 @@ ROW_ALIGN = 64  # fp32 elements: every peer row of a plane starts a 256-B bounda
 
 def plane_count(k: int, n: int, at_least: int = 1) -> int:
     """Chunks S >= at_least that split n coordinates evenly (n % S == 0) into
-    planes of k rows spanning <= PLANE_BYTES each (the first such S; n itself
-    when nothing smaller divides it)."""
-    s = max(at_least, -(-(k * n * 4) // PLANE_BYTES), 1)
-    while n % s:
-        s += 1
-    return s
+    planes of k rows spanning <= PLANE_BYTES each: the first such S up to 64
+    times the smallest that fits (ValueError past that -- pad n)."""
+    s0 = max(at_least, -(-(k * n * 4) // PLANE_BYTES), 1)
+    for s in range(s0, min(n, 64 * s0) + 1):
+        if n % s == 0:
+            return s
+    raise ValueError(f"no chunk count in [{s0}, {64 * s0}] divides {n} coordinates evenly")
 
 
 class PeerPlanes:

@@ -45,6 +45,11 @@ def test_plane_count(k, n, at_least, want):
     assert s == 1 or k * (n // s) * 4 <= sharded.PLANE_BYTES or s == n
 
 
+def test_plane_count_refuses_an_unsplittable_size():
+    with pytest.raises(ValueError, match="divides"):
+        sharded.plane_count(256, 1_000_000_007)  # prime, 128 GB: no even split near 8 planes
+
+
 @pytest.mark.gpu
 def test_peer_planes_layout_and_reduce(cuda):
     """PeerPlanes: chunk-major planes, 256-B aligned rows, one table per
