@@ -99,7 +99,8 @@ class PeerPlanes:
         round s's all-gather writes every rank's chunk s to the contiguous
         w_full[s*G*C, (s+1)*G*C): on ``comm`` (a second stream) beside plane
         s+1's reduction, the compute stream waiting for the last one; without
-        ``comm``, in line.  ``hook(s, phase, stream)`` runs at "reduce0" /
+        ``comm``, in line.  Without a process group (one rank), chunk s is
+        copied to w_full[s*C, (s+1)*C).  ``hook(s, phase, stream)`` runs at "reduce0" /
         "reduce1" / "gather0" / "gather1" on the stream of that step (timing
         events); ``reduce(planes, s, w, rule, lr, trim_frac)`` replaces the HIP
         reduction (the CPU gloo tests)."""
@@ -108,7 +109,7 @@ class PeerPlanes:
         gather = w_full is not None and dist.is_initialized()
         G = dist.get_world_size(group) if gather else 1
         C = self.chunk
-        if gather and w_full.numel() < self.chunks * G * C:
+        if w_full is not None and w_full.numel() < self.chunks * G * C:
             raise ValueError(f"w_full has {w_full.numel()} elements, the round needs {self.chunks * G * C}")
         comp = torch.cuda.current_stream(self.data.device) if self.data.is_cuda else None
         for s in range(self.chunks):
@@ -121,6 +122,8 @@ class PeerPlanes:
             if hook:
                 hook(s, "reduce1", comp)
             if not gather:
+                if w_full is not None:
+                    w_full[s * C:(s + 1) * C].copy_(ws[s])
                 continue
             out = w_full[s * G * C:(s + 1) * G * C]
             if comm is not None:

@@ -194,6 +194,25 @@ def test_gloo_peer_planes_round_byte_identical_to_single(world, rule, n, k, S):
     assert all(got[r] == want.tobytes() for r in range(world))
 
 
+def test_peer_planes_one_rank_fills_w_full():
+    """No process group: each plane's chunk lands at w_full[s*C:(s+1)*C]."""
+    k, S, C = 4, 3, 50
+    peers = [oracle.synth(S * C, 31, p, 1e-2) for p in range(k)]
+    w = oracle.synth(S * C, 31, 0xFFFFF, 5e-2)
+    planes = sharded.PeerPlanes(k, S, C, "cpu")
+    for s in range(S):
+        for p in range(k):
+            planes.row(s, p).copy_(torch.from_numpy(peers[p][s * C:(s + 1) * C]))
+    ws = [torch.from_numpy(w[s * C:(s + 1) * C].copy()) for s in range(S)]
+    w_full = torch.zeros(S * C)
+    planes.aggregate_gather_(ws, w_full, reduce=lambda pl, s, wc, r, lr, tf: oracle_reduce(
+        [pl.row(s, p) for p in range(pl.k)], wc, r, lr, tf))
+    want, _ = oracle.fedavg(peers, w)
+    assert w_full.numpy().tobytes() == want.tobytes()
+    with pytest.raises(ValueError, match="w_full"):
+        planes.aggregate_gather_(ws, torch.zeros(S * C - 1), reduce=lambda *a: None)
+
+
 def test_peer_planes_checks_round_shapes():
     planes = sharded.PeerPlanes(3, 2, 10, "cpu")
     with pytest.raises(ValueError, match="w chunks"):
