@@ -635,7 +635,9 @@ def test_robust_float_fast_path_specials(cuda, rule, k, nan_stripe):
 @pytest.mark.parametrize("k", [16, 64, 100, 128, 200, 256])
 def test_robust_single_nan_at_every_peer_position(cuda, rule, k):
     """The float networks' NaN test (robust_nets.h nan_lanes: packed-FMA
-    chains ended by one compare) must see a NaN wherever it sits: tile t
+    chains ended by one compare; the pair kernels, K > 128: one compare of
+    the sort's rank-0 output, its cone all v_minimum3) must see a NaN
+    wherever it sits: tile t
     (64 coordinates, one wave / pair block) holds exactly one NaN, at peer t,
     in lane 7t mod 64 -- every peer position of every chain is hit once, with
     both signs and a payload -- among values whose products overflow in other
