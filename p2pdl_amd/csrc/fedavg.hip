@@ -241,7 +241,10 @@ __global__ __launch_bounds__(kBlock) void fedavg_flat_kernel(const float* const*
 // TB/s with this access pattern.
 constexpr int kSL = 4;                       // loader waves
 constexpr int kSC = 8;                       // consumer waves
-constexpr int kSS = 3;                       // ring stages (+ w: 128 KiB of LDS)
+#ifndef P2P_SPLIT_STAGES
+#define P2P_SPLIT_STAGES 3  // (an A/B build may set 4: 160 KiB of LDS)
+#endif
+constexpr int kSS = P2P_SPLIT_STAGES;        // ring stages (+ w: 128 KiB of LDS)
 constexpr int kSTile = 8192;                 // floats per tile (32 KiB per peer)
 constexpr int kSPer = kSTile / 256 / kSL;    // DMA instructions per loader per stage
 constexpr int kSRpw = kSTile / 256 / kSC;    // ds_read_b128 per consumer lane per stage
