@@ -364,6 +364,20 @@ def _nccl_world1_worker(port, q):
             sharded_aggregate_(w, peers, rule=rule, chunk=chunk)
             torch.cuda.synchronize()
             out[rule] = (w.cpu().numpy().tobytes(), dist.get_backend())
+        # the memory-sharded plane round: HIP reduce per plane, each plane's
+        # RCCL all-gather on a second stream beside the next plane
+        k, S, C = 20, 3, 70_001
+        planes = sharded.PeerPlanes(k, S, C, dev)
+        peers = [oracle.synth(S * C, 37, p, 1e-2) for p in range(k)]
+        w = oracle.synth(S * C, 37, 0xFFFFF, 5e-2)
+        for s_ in range(S):
+            for p in range(k):
+                planes.row(s_, p).copy_(torch.from_numpy(peers[p][s_ * C:(s_ + 1) * C]))
+        ws = [torch.from_numpy(w[s_ * C:(s_ + 1) * C].copy()).to(dev) for s_ in range(S)]
+        w_full = torch.zeros(S * C, dtype=torch.float32, device=dev)
+        planes.aggregate_gather_(ws, w_full, rule="fedavg", comm=torch.cuda.Stream(dev))
+        torch.cuda.synchronize()
+        out["planes"] = (w_full.cpu().numpy().tobytes(), dist.get_backend())
         q.put(out)
         dist.destroy_process_group()
     except BaseException as e:  # report, do not hang the parent
@@ -388,3 +402,6 @@ def test_gpu_world1_nccl_allgather_path(cuda):
         w = oracle.synth(n, 29, 0xFFFFF, 5e-2)
         want = oracle.fedavg(peers, w)[0] if rule == "fedavg" else oracle.robust(peers, 1, 0, w=w)[0]
         assert b == want.tobytes(), rule
+    b, backend = got["planes"]
+    peers = [oracle.synth(3 * 70_001, 37, p, 1e-2) for p in range(20)]
+    assert backend == "nccl" and b == oracle.fedavg(peers, oracle.synth(3 * 70_001, 37, 0xFFFFF, 5e-2))[0].tobytes()
