@@ -639,13 +639,16 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
             call(record=True)
         torch.cuda.synchronize()
         ev_fast = list(ev)
-        # the segment kernel alone: the launch aggregate_models cached on the
+        # the kernel alone: the launch aggregate_models cached on the
         # validated model-state entry (ops.relaunch: no table work), queued
         # behind a spin so no host time falls between the events
         from p2pdl_amd.aggregator.model_state import model_state
 
         _, ws_m, st_m = model_state(model)
         launch = st_m.extra.get("launch") if st_m is not None else None
+        kernel_path = (("split kernel over the slab rows as flat peers (ops._rows_entry)"
+                        if launch[2][5][0] == "rows" else "VGPR segment kernel (+ split tiles when planned)")
+                       if launch is not None else "general path")
         kernel_ms = None
         if launch is not None:
             kernel_ms = kernel_only_ms(lambda: ops.relaunch(launch[2], dev, len(ws_m), K, 0.1), steps, comp)
@@ -701,7 +704,8 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
                   | ({"reference_on_gpu_us_per_call": round(ref_s * 1e6, 1),
                       "speedup_vs_reference_on_gpu": round(ref_s / step_s, 1)} if ref_s else {}),
         "roofline": roofline(4 * n * (K + 2), kernel_ms or call_ms, traffic_for(name, n, K),
-                             timing=("the segment kernel alone: HIP events around the cached launch "
+                             kernel_path=kernel_path,
+                             timing=("the kernel alone: HIP events around the cached launch "
                                      "(ops.relaunch) queued behind a spin kernel; call_ms: events around the "
                                      "whole aggregate_models call; value / us_per_call: host wall time, no events"
                                      if kernel_ms else "HIP events around aggregate_models (no cached launch)"),

@@ -40,8 +40,10 @@ extern "C" {
  * 5: P2P_DELTA_TILE 4096 -> 1024 (the delta segment table's tile_begin is
  *    counted in 1024-element tiles).
  * 6: adds p2p_fedavg_split_plan / p2p_fedavg_split_segments_f32 (whole
- *    tiles of a state_dict on the LDS-DMA split kernel). */
-#define P2P_ABI_VERSION 6
+ *    tiles of a state_dict on the LDS-DMA split kernel).
+ * 7: adds p2p_fedavg_split_rows_f32 / p2p_row_chunk_t (a state_dict slab's
+ *    rows as flat peers, the model scattered by 1024-float chunks). */
+#define P2P_ABI_VERSION 7
 
 typedef void *p2p_stream_t; /* hipStream_t */
 
@@ -136,6 +138,24 @@ typedef struct p2p_split_tile_t {
 int64_t p2p_fedavg_split_plan(int32_t k, int64_t full_tiles);
 int32_t p2p_fedavg_split_segments_f32(const p2p_split_tile_t *tiles, int64_t ntiles, const p2p_segment_t *segs,
                                       int32_t k, int32_t rule, float lr, p2p_stream_t stream);
+
+/* FedAvg over the K rows of a state_dict slab (node/inbox.py DeviceInbox) on
+ * the split kernel, one launch, every tile whole: `rows` is a DEVICE array of
+ * K row pointers (16-B aligned) each holding ntiles * P2P_SPLIT_TILE floats;
+ * chunks[c] (DEVICE, ntiles * 8 entries) is the model tensor memory the
+ * row's floats [P2P_ROW_CHUNK * c, + P2P_ROW_CHUNK) update -- `w` 16-B
+ * aligned, `valid` how many of the chunk's floats it holds (<= 1024, 0 or w
+ * NULL for padding between keys, which is averaged and dropped).  The
+ * model's keys must therefore start on P2P_ROW_CHUNK boundaries of the row.
+ * w[i] += lr * mean_k(row_k[c0 + i]) with the same per-element op order as
+ * p2p_fedavg_apply_f32 (FedAvg rules only). */
+#define P2P_ROW_CHUNK 1024
+typedef struct {
+  float *w;
+  int64_t valid;
+} p2p_row_chunk_t;
+int32_t p2p_fedavg_split_rows_f32(const float *const *rows, int32_t k, int64_t ntiles, const p2p_row_chunk_t *chunks,
+                                  int32_t rule, float lr, p2p_stream_t stream);
 
 /* Whole state_dict in ONE launch: segs is a DEVICE array of nseg entries
  * (tile_begin prefix-summed with p2p_tile_elems(rule, k)); total_tiles is the

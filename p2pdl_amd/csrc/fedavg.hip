@@ -291,21 +291,75 @@ __device__ __forceinline__ SplitTile split_tile(const float* const* peers, float
   }
 }
 
+// One ROWS tile of consumer wave cw: its chunk's w slice DMA'd beside the
+// stages (lanes inside the chunk's valid floats only), the K stages added in
+// peer order, then / K and the apply where the chunk holds model floats --
+// element-wise for the float4 that straddles the key's end.
+template <bool RECIP>
+__device__ __forceinline__ void rows_tile(const p2p_row_chunk_t* ch, int K, int lane, float lr, float fk, float inv,
+                                          float* lds, uint32_t lds0, uint32_t mine, int& slot, int cw) {
+  float* cwp = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&ch->w))));
+  const int64_t valid = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&ch->valid))));
+  if (cwp) {
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r) {
+      const int idx = lane * 4 + r * 256;
+      if (idx + 4 <= valid) dma16<0>(cwp + idx, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
+    }
+  }
+  f4 acc[kSRpw];
+#pragma unroll
+  for (int r = 0; r < kSRpw; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
+  for (int k = 0; k < K; ++k) {
+    __builtin_amdgcn_s_barrier();
+    f4 x[kSRpw];
+    lds_read4(x, lds0 + static_cast<uint32_t>(slot) * (kSTile * 4) + mine);
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r) acc[r] += x[r];  // strictly in list order (:25-28)
+    slot = slot + 1 == kSS ? 0 : slot + 1;
+  }
+  if (!cwp) return;  // padding between keys: averaged, dropped
+  f4 m[kSRpw];
+#pragma unroll
+  for (int r = 0; r < kSRpw; ++r) m[r] = div4<RECIP>(acc[r], fk, inv);  // (:31-32)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w DMA (and its older stores)
+  f4 wq[kSRpw];
+  lds_read4(wq, lds0 + static_cast<uint32_t>(kSS * kSTile * 4) + mine);
+#pragma unroll
+  for (int r = 0; r < kSRpw; ++r) {
+    const int idx = lane * 4 + r * 256;
+    if (idx + 4 <= valid) {
+      st(cwp + idx, apply4(wq[r], lr, m[r]));  // (:36-38)
+    } else if (idx < valid) {  // the key's last, partial float4
+      const float mv[4] = {m[r].x, m[r].y, m[r].z, m[r].w};
+      for (int e = 0; idx + e < valid; ++e) stg(cwp + idx + e, apply_lr(ldg(cwp + idx + e), lr, mv[e]));
+    }
+  }
+}
+
 // SEGS: the host lists only whole tiles of segments whose K peer pointers and
 // w / out are all 16-B aligned (ops.py checks them when it builds the list);
 // a flat buffer is checked here.
-template <bool RECIP, bool SEGS>
+// ROWS (round 5): the peers are the K rows of a state_dict slab (DeviceInbox)
+// read as flat buffers -- every tile a whole one -- and the model is
+// scattered: consumer wave c of tile t applies to chunks[8t + c], the w
+// tensor (if any) holding the row's floats [1024(8t + c), +1024) and how
+// many of them it holds (keys start on 1024-float boundaries; the padding
+// between them is averaged and dropped).  The host checks the alignment.
+template <bool RECIP, bool SEGS, bool ROWS = false>
 __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const float* const* __restrict__ peers,
                                                                         int K, const int32_t* k_dev,
                                                                         int64_t ntiles, float* w, float* out,
                                                                         float lr, const p2p_split_tile_t* tiles,
-                                                                        const Seg* segs) {
+                                                                        const Seg* segs,
+                                                                        const p2p_row_chunk_t* chunks = nullptr) {
+  static_assert(!(SEGS && ROWS), "one mode");
   __shared__ __attribute__((aligned(16))) float lds[(kSS + 1) * kSTile];
   if (k_dev) K = __builtin_amdgcn_readfirstlane(ldg(k_dev));
   if (K <= 0) return;
   const int64_t G = gridDim.x, b = bid_x();
   const int wv = __builtin_amdgcn_readfirstlane(tid_x() >> 6), lane = tid_x() & 63;
-  if (!SEGS && !all_aligned16(peers, K, w, out)) {
+  if (!SEGS && !ROWS && !all_aligned16(peers, K, w, out)) {
     // 4-B-aligned views: element-wise, same op order, no LDS (block-uniform)
     constexpr int kT = 64 * (kSL + kSC);
     for (int64_t t = b; t < ntiles; t += G)  // 11 x 768 >= 8192: the tile's end bounds the last
@@ -342,6 +396,10 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
   const float inv = RECIP ? 1.0f / fk : 0.f;
   int slot = 0;
   for (int64_t t = b; t < ntiles; t += G) {
+    if constexpr (ROWS) {
+      rows_tile<RECIP>(chunks + t * kSC + cw, K, lane, lr, fk, inv, lds, lds0, mine, slot, cw);
+      continue;
+    }
     const SplitTile tl = split_tile<SEGS>(peers, w, out, tiles, segs, t);
     const int64_t o = tl.c0 + cw * kSRpw * 256 + lane * 4;
     if (tl.w) {
@@ -482,8 +540,25 @@ static int32_t launch_status() {
 extern "C" P2P_INTERNAL int64_t p2p_fedavg_tile_elems(void) { return kTile; }
 
 static_assert(kSTile == P2P_SPLIT_TILE, "the ABI's split tile");
+static_assert(kSRpw * 256 == P2P_ROW_CHUNK && kSC * P2P_ROW_CHUNK == kSTile, "a consumer wave's chunk");
 
 extern "C" int64_t p2p_fedavg_split_plan(int32_t k, int64_t full_tiles) { return split_tiles_for(k, full_tiles); }
+
+extern "C" int32_t p2p_fedavg_split_rows_f32(const float* const* rows, int32_t k, int64_t ntiles,
+                                            const p2p_row_chunk_t* chunks, int32_t rule, float lr,
+                                            p2p_stream_t stream) {
+  if (!rows || !chunks || k < 1 || ntiles < 1) return P2P_ERR_INVALID;
+  if (rule != P2P_RULE_FEDAVG && rule != P2P_RULE_FEDAVG_TORCH_GPU) return P2P_ERR_INVALID;
+  const dim3 grid = split_grid(ntiles), block(64 * (kSL + kSC));
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  if (rule == P2P_RULE_FEDAVG_TORCH_GPU)
+    hipLaunchKernelGGL((fedavg_split_kernel<true, false, true>), grid, block, 0, st, rows, k, nullptr, ntiles, nullptr,
+                       nullptr, lr, nullptr, nullptr, chunks);
+  else
+    hipLaunchKernelGGL((fedavg_split_kernel<false, false, true>), grid, block, 0, st, rows, k, nullptr, ntiles,
+                       nullptr, nullptr, lr, nullptr, nullptr, chunks);
+  return launch_status();
+}
 
 extern "C" int32_t p2p_fedavg_split_segments_f32(const p2p_split_tile_t* tiles, int64_t ntiles,
                                                  const p2p_segment_t* segs, int32_t k, int32_t rule, float lr,

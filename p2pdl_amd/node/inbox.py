@@ -760,6 +760,11 @@ class LandedUpdate(OrderedDict):
 
 
 ROW_ALIGN = 64  # fp32 elements (256 B) per tensor offset in a slab row
+# The chunk layout (round 5): every key on a 1024-float boundary and the row
+# pitch whole 8192-float tiles, so FedAvg can read the rows as flat peers on
+# the split kernel (ops._rows_entry, include/p2pdl.h p2p_fedavg_split_rows_f32)
+# -- taken when it pads the row by at most CHUNK_PAD_MAX.
+ROW_CHUNK, ROW_TILE, CHUNK_PAD_MAX = 1024, 8192, 0.05
 
 
 class _Consuming:
@@ -806,16 +811,23 @@ class DeviceInbox:
                  pool_bytes: int | None = None):
         self.device = torch.device(device) if device is not None else next(
             (t.device for t in template.values() if t.is_cuda), torch.device("cuda", torch.cuda.current_device()))
-        self.layout = OrderedDict()
-        off = 0
-        for key, t in template.items():
-            if t.dtype == torch.float32:
-                # 256-B aligned offsets (and row pitch): every tensor view starts
-                # a 128-B HBM line, as a separate allocation would -- a 16-B
-                # aligned view straddles one more line per kernel tile
-                self.layout[key] = (off, tuple(t.shape), t.numel())
-                off += -(-t.numel() // ROW_ALIGN) * ROW_ALIGN
-        self.row = off
+        # 256-B aligned offsets (and row pitch): every tensor view starts a
+        # 128-B HBM line, as a separate allocation would -- a 16-B aligned
+        # view straddles one more line per kernel tile.  The chunk layout
+        # (1024-float offsets, whole-tile pitch) when it costs <= 5% of the row.
+        f32 = [(key, t) for key, t in template.items() if t.dtype == torch.float32]
+
+        def place(align, pitch_to):
+            lay, off = OrderedDict(), 0
+            for key, t in f32:
+                lay[key] = (off, tuple(t.shape), t.numel())
+                off += -(-t.numel() // align) * align
+            return lay, -(-off // pitch_to) * pitch_to if off else 0
+
+        self.layout, self.row = place(ROW_ALIGN, ROW_ALIGN)
+        chunked, crow = place(ROW_CHUNK, ROW_TILE)
+        if crow <= (1 + CHUNK_PAD_MAX) * self.row:
+            self.layout, self.row = chunked, crow
         self.k_max = int(k_max)
         self.slab = torch.empty((self.k_max, self.row), dtype=torch.float32, device=self.device)
         self._stage = [torch.empty(self.row, dtype=torch.float32, pin_memory=True) for _ in range(2)]

@@ -374,11 +374,67 @@ def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_fra
     return None
 
 
+ROW_CHUNK = 1024  # == P2P_ROW_CHUNK
+_CHUNK_DTYPE = np.dtype([("w", "<u8"), ("valid", "<i8")])  # == p2p_row_chunk_t (16 B)
+
+
+def _rows_entry(ws, w_ptrs, numels, slab, rows_a, offs_a, r, K, lr, dev, cache_key):
+    """FedAvg over slab rows as flat peers (include/p2pdl.h
+    p2p_fedavg_split_rows_f32): one split launch over whole tiles of the rows,
+    the model scattered by 1024-float chunks.  Taken when every key starts a
+    1024-float boundary (DeviceInbox's chunk layout), the rows hold whole
+    tiles, the w tensors are 16-B aligned and the tiles fill at least one
+    round of the CUs (the split plan); otherwise None (the segment path)."""
+    if r not in FEDAVG_RULES:
+        return None
+    n_a = np.asarray(numels, dtype=np.int64)
+    if (offs_a % ROW_CHUNK).any() or (np.asarray(w_ptrs, dtype=np.uint64) % np.uint64(16)).any():
+        return None
+    width = slab.shape[1]
+    ntiles = -(-int((offs_a + n_a).max()) // SPLIT_TILE)
+    if ntiles * SPLIT_TILE > width or (width * 4) % 16 or slab.data_ptr() % 16:
+        return None
+    if int(N.lib().p2p_fedavg_split_plan(K, ntiles)) <= 0:  # below one round (or K < 16)
+        return None
+    order = np.argsort(offs_a, kind="stable")
+    ends = offs_a[order] + n_a[order]
+    if (offs_a[order][1:] < ends[:-1]).any():  # overlapping keys: no chunk map
+        return None
+    chunks = np.zeros(ntiles * (SPLIT_TILE // ROW_CHUNK), dtype=_CHUNK_DTYPE)
+    for l in range(len(ws)):
+        n = int(n_a[l])
+        if n == 0:
+            continue
+        c0, c1 = int(offs_a[l]) // ROW_CHUNK, -(-(int(offs_a[l]) + n) // ROW_CHUNK)
+        j = np.arange(c1 - c0, dtype=np.int64)
+        chunks["w"][c0:c1] = np.uint64(w_ptrs[l]) + (j * ROW_CHUNK * 4).astype(np.uint64)
+        chunks["valid"][c0:c1] = np.minimum(ROW_CHUNK, n - j * ROW_CHUNK)
+    row_ptrs = np.uint64(slab.data_ptr()) + rows_a.astype(np.uint64) * np.uint64(width * 4)
+    host = np.concatenate([row_ptrs.view(np.uint8), chunks.view(np.uint8)])
+    buf = torch.empty(host.nbytes, dtype=torch.uint8, device=dev)
+    _RING.to_device(host, dev, out=buf)
+    entry = (buf, 0, r, 0, torch.cuda.current_stream(dev).cuda_stream, ("rows", row_ptrs.nbytes, ntiles))
+    with torch.cuda.device(dev):
+        _launch_entry(entry, K, lr, N.stream_handle())
+    with _TABLES_LOCK:
+        _TABLES[cache_key] = entry
+        while len(_TABLES) > _TABLES_MAX:
+            _TABLES.popitem(last=False)
+    return entry
+
+
 def _launch_entry(entry, K: int, lr: float, stream) -> None:
-    """The launches of one segment-table entry: the split kernel over its
-    tile list (when planned), then the VGPR segment kernel over the rest."""
-    buf, tiles, r, b, _, (rem_off, Lr, split) = entry
+    """The launches of one segment-table entry: the rows kernel (a slab's rows
+    as flat peers), or the split kernel over its tile list (when planned),
+    then the VGPR segment kernel over the rest."""
+    buf, tiles, r, b, _, extra = entry
     base = buf.data_ptr()
+    if extra[0] == "rows":
+        _, ch_off, ntiles = extra
+        N.check(N.lib().p2p_fedavg_split_rows_f32(base, K, ntiles, base + ch_off, r, lr, stream),
+                "p2p_fedavg_split_rows_f32")
+        return
+    rem_off, Lr, split = extra
     if split is not None:
         lst_off, S, segs_off = split
         N.check(N.lib().p2p_fedavg_split_segments_f32(base + lst_off, S, base + segs_off, K, r, lr, stream),
@@ -510,6 +566,9 @@ def aggregate_slab_rows_(ws: Sequence[torch.Tensor], slab: torch.Tensor, rows: S
         raise IndexError("slab row out of range")
     if offs_a.min() < 0 or (offs_a + np.asarray(numels, dtype=np.int64)).max() > width:
         raise IndexError("segment outside the slab row")
+    entry = _rows_entry(ws, w_ptrs, numels, slab, rows_a, offs_a, rule_id(rule), K, lr, dev, key)
+    if entry is not None:
+        return entry
     base, stride = slab.data_ptr(), width * 4
     ptrs = (np.uint64(base) + rows_a.astype(np.uint64)[None, :] * np.uint64(stride)
             + offs_a.astype(np.uint64)[:, None] * np.uint64(4))

@@ -313,6 +313,64 @@ def test_fedavg_split_segments_at_the_product_gate(cuda):
         assert_bits_equal(host(ws[l]), want[l], what=f"segment {l} w")
 
 
+ROWS_SIZES = [2_300_001, 100, 1023, 1024, 1025, 9 * 64 * 9, 300_001, 3, 4096, 8191]
+
+
+@pytest.mark.parametrize("k,rule", [(16, "fedavg"), (20, "fedavg_torch_gpu"), (64, "fedavg")])
+def test_slab_rows_split_path_vs_oracle(cuda, k, rule, monkeypatch):
+    """DeviceInbox's chunk layout (keys on 1024-float boundaries, whole-tile
+    pitch) sends FedAvg down the rows kernel (ops._rows_entry: the slab rows
+    as flat peers, the model scattered by chunk): bit-exact per key against
+    the oracle, keys ending mid-chunk and mid-float4 included, NaN in every
+    row's padding ignored, and again through the cached relaunch."""
+    from p2pdl_amd.node.inbox import DeviceInbox
+
+    template = {f"t{i}": torch.zeros(n, device=cuda) for i, n in enumerate(ROWS_SIZES)}
+    inbox = DeviceInbox(template, k_max=k, device=cuda)
+    offs = [inbox.layout[f"t{i}"][0] for i in range(len(ROWS_SIZES))]
+    assert all(o % 1024 == 0 for o in offs) and inbox.row % 8192 == 0
+    seed = 0x7035 + k
+    for j in range(k):
+        ops.fill_synthetic_(inbox.slab[j], seed, j, 1e-2)
+    pad = torch.ones(inbox.row, dtype=torch.bool, device=cuda)
+    for o, n in zip(offs, ROWS_SIZES):
+        pad[o:o + n] = False
+    inbox.slab[:k, pad] = float("nan")  # padding: averaged and dropped
+    ws = []
+    for i, n in enumerate(ROWS_SIZES):
+        w = torch.empty(n, dtype=torch.float32, device=cuda)
+        ops.fill_synthetic_(w, seed + 1, i, 5e-2)
+        ws.append(w)
+    rows_host = inbox.slab[:k].cpu().numpy()
+    want = [host(w) for w in ws]
+
+    def boom(*a, **kw):
+        raise AssertionError("segment path taken")
+
+    monkeypatch.setattr(ops, "_launch_segments", boom)
+    ops._TABLES.clear()
+    for rnd in range(2):  # the second call: the cached entry's relaunch
+        ops.aggregate_slab_rows_(ws, inbox.slab, list(range(k)), offs, rule)
+        for l, (o, n) in enumerate(zip(offs, ROWS_SIZES)):
+            want[l], _ = oracle.fedavg([rows_host[j, o:o + n] for j in range(k)], want[l],
+                                       torch_gpu=rule == "fedavg_torch_gpu")
+            assert_bits_equal(host(ws[l]), want[l], what=f"round {rnd} key {l} ({n} floats)")
+
+
+def test_slab_rows_path_needs_k16_and_a_round(cuda):
+    """Below 16 peers, or below one round of tiles, the slab keeps the
+    segment path (the rows entry declines)."""
+    from p2pdl_amd.node.inbox import DeviceInbox
+
+    template = {"a": torch.zeros(100_000, device=cuda), "b": torch.zeros(5, device=cuda)}
+    inbox = DeviceInbox(template, k_max=16, device=cuda)
+    ws = [torch.zeros(100_000, device=cuda), torch.zeros(5, device=cuda)]
+    offs = [inbox.layout["a"][0], inbox.layout["b"][0]]
+    rows_a, offs_a = np.arange(16), np.asarray(offs)
+    assert ops._rows_entry(ws, [w.data_ptr() for w in ws], (100_000, 5), inbox.slab, rows_a, offs_a, 0, 16,
+                           0.1, cuda, ("t",)) is None  # 13 tiles < one round
+
+
 def test_split_plan_takes_whole_rounds_of_aligned_tiles(cuda, monkeypatch):
     """The plan itself (host logic): whole tiles of aligned segments only, in
     segment order, whole rounds of the CU count; each segment's rest is its
