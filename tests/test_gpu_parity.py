@@ -357,6 +357,39 @@ def test_slab_rows_split_path_vs_oracle(cuda, k, rule, monkeypatch):
             assert_bits_equal(host(ws[l]), want[l], what=f"round {rnd} key {l} ({n} floats)")
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_slab_rows_random_layouts(cuda, seed):
+    """Random state_dict shapes (1..1100 floats and a few large tensors, random
+    key order) through DeviceInbox's chunk layout and the rows kernel, K = 16:
+    every key bit-exact against the oracle."""
+    from p2pdl_amd.node.inbox import DeviceInbox
+
+    rng = np.random.default_rng(seed)
+    sizes = list(rng.integers(1, 1100, size=40)) + list(rng.integers(450_000, 900_000, size=5))
+    rng.shuffle(sizes)
+    k = 16
+    template = {f"k{i}": torch.zeros(int(n), device=cuda) for i, n in enumerate(sizes)}
+    inbox = DeviceInbox(template, k_max=k, device=cuda)
+    offs = [inbox.layout[f"k{i}"][0] for i in range(len(sizes))]
+    if not all(o % 1024 == 0 for o in offs):
+        pytest.skip("layout fell back to 64-float alignment (padding > 5%)")
+    for j in range(k):
+        ops.fill_synthetic_(inbox.slab[j], 0x7040 + seed, j, 1e-2)
+    ws = []
+    for i, n in enumerate(sizes):
+        w = torch.empty(int(n), dtype=torch.float32, device=cuda)
+        ops.fill_synthetic_(w, 0x7041 + seed, i, 5e-2)
+        ws.append(w)
+    rows_host = inbox.slab[:k].cpu().numpy()
+    want = [oracle.fedavg([rows_host[j, o:o + int(n)] for j in range(k)], host(w))[0]
+            for o, n, w in zip(offs, sizes, ws)]
+    ops._TABLES.clear()
+    entry = ops.aggregate_slab_rows_(ws, inbox.slab, list(range(k)), offs, "fedavg")
+    assert entry is not None and entry[5][0] == "rows"
+    for l in range(len(sizes)):
+        assert_bits_equal(host(ws[l]), want[l], what=f"seed {seed} key {l} ({sizes[l]} floats)")
+
+
 def test_slab_rows_path_needs_k16_and_a_round(cuda):
     """Below 16 peers, or below one round of tiles, the slab keeps the
     segment path (the rows entry declines)."""
