@@ -118,6 +118,8 @@ def aggregate(peers: Sequence[torch.Tensor], rule="fedavg", *, w: torch.Tensor |
     b = 0
     if r == P2P_RULE_TRIMMED:
         b = trim_count(k, trim_frac) if trim_b is None else int(trim_b)
+    if n == 0:  # nothing to reduce (the reference's loops over empty tensors); an empty
+        return  # tensor's data pointer is NULL, which the C ABI would refuse
     with torch.cuda.device(ref.device):
         N.check(N.lib().p2p_aggregate_f32(table.data_ptr(), k, n, r, b, lr,
                                           w.data_ptr() if w is not None else None,
@@ -147,6 +149,8 @@ def fedavg16_apply_(w: torch.Tensor, peers: Sequence[torch.Tensor], rule="fedavg
         if p.dtype != w.dtype or p.device != w.device or not p.is_contiguous() or p.numel() != w.numel():
             raise ValueError(f"peers[{i}]: expected a contiguous {w.dtype} tensor of {w.numel()} elements on "
                              f"{w.device}, got {p.dtype} {p.numel()} on {p.device}")
+    if w.numel() == 0:  # nothing to do; an empty tensor's data pointer is NULL
+        return
     table = pointer_table(peers, w.device)
     with torch.cuda.device(w.device):
         N.check(N.lib().p2p_fedavg_apply_16(table.data_ptr(), len(peers), w.numel(), w.data_ptr(), lr, dt, r,
@@ -184,6 +188,8 @@ def apply_(w: torch.Tensor, agg: torch.Tensor, lr: float = 0.1) -> torch.Tensor:
     _check_f32(agg, "agg", w.device)
     if agg.numel() != w.numel():
         raise ValueError("w and agg differ in size")
+    if w.numel() == 0:
+        return w
     with torch.cuda.device(w.device):
         N.check(N.lib().p2p_apply_f32(w.data_ptr(), agg.data_ptr(), lr, w.numel(),
                                       N.stream_handle()), "p2p_apply_f32")
@@ -607,6 +613,8 @@ def delta_snapshot_(cur: torch.Tensor, prev: torch.Tensor, delta: torch.Tensor, 
         _check_f32(t, name, cur.device)
         if t.numel() != cur.numel():
             raise ValueError(f"{name} has {t.numel()} elements, expected {cur.numel()}")
+    if cur.numel() == 0:
+        return
     with torch.cuda.device(cur.device):
         N.check(N.lib().p2p_delta_snapshot_f32(cur.data_ptr(), prev.data_ptr(), delta.data_ptr(), cur.numel(),
                                                int(first), N.stream_handle()), "p2p_delta_snapshot_f32")
@@ -750,6 +758,8 @@ def fedavg_apply_devk_(w: torch.Tensor, table: torch.Tensor, k_dev: torch.Tensor
     _check_tensor(table, "table", (torch.int64, torch.uint64), None, dev, min_numel=k_max)
     table_covers(table, w.numel())
     _check_tensor(k_dev, "k_dev", torch.int32, None, dev, min_numel=1)
+    if w.numel() == 0:
+        return
     with torch.cuda.device(w.device):
         N.check(N.lib().p2p_fedavg_apply_devk_f32(table.data_ptr(), k_dev.data_ptr(), k_max, w.numel(),
                                                   w.data_ptr(), lr,
@@ -762,6 +772,8 @@ def fill_synthetic_(out: torch.Tensor, seed: int, peer: int, scale: float, chunk
                     nranks: int = 1, rank: int = 0) -> torch.Tensor:
     N.require_device(out)
     _check_f32(out, "out", out.device)
+    if out.numel() == 0:
+        return out
     with torch.cuda.device(out.device):
         N.check(N.lib().p2p_fill_synthetic_f32(out.data_ptr(), out.numel(), seed, peer, scale,
                                                chunk, nranks, rank, N.stream_handle()),

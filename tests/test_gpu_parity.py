@@ -390,6 +390,46 @@ def test_slab_rows_random_layouts(cuda, seed):
         assert_bits_equal(host(ws[l]), want[l], what=f"seed {seed} key {l} ({sizes[l]} floats)")
 
 
+@pytest.mark.parametrize("rule", ["fedavg", "median", "trimmed"])
+def test_zero_size_tensors(cuda, rule):
+    """Empty inputs as the reference's loops see them (nothing to add):
+    a flat call over 0 coordinates, and a zero-size key inside a state_dict
+    -- through the segment table and through DeviceInbox's rows kernel --
+    leave every other key bit-exact and raise nothing."""
+    from p2pdl_amd.node.inbox import DeviceInbox
+
+    k = 16
+    r = ops.rule_id(rule)
+    b = ops.trim_count(k) if r == 2 else 0
+    empty = [torch.zeros(0, device=cuda) for _ in range(k)]
+    w0 = torch.zeros(0, device=cuda)
+    ops.aggregate(empty, rule, w=w0)
+    if r == 0:
+        ops.fedavg16_apply_(w0.half(), [e.half() for e in empty])
+        ops.delta_snapshot_(w0, torch.zeros(0, device=cuda), torch.zeros(0, device=cuda))
+        ops.apply_(w0, torch.zeros(0, device=cuda))
+        ops.fill_synthetic_(w0, 1, 2, 1.0)
+    sizes = [2_200_000, 0, 777]
+    template = {f"t{i}": torch.zeros(n, device=cuda) for i, n in enumerate(sizes)}
+    inbox = DeviceInbox(template, k_max=k, device=cuda)
+    offs = [inbox.layout[f"t{i}"][0] for i in range(len(sizes))]
+    for j in range(k):
+        ops.fill_synthetic_(inbox.slab[j], 0x7050, j, 1e-2)
+    ws = [torch.empty(n, dtype=torch.float32, device=cuda) for n in sizes]
+    for i, w in enumerate(ws):
+        if w.numel():
+            ops.fill_synthetic_(w, 0x7051, i, 5e-2)
+    rows_host = inbox.slab[:k].cpu().numpy()
+    want = []
+    for o, n, w in zip(offs, sizes, ws):
+        peers = [rows_host[j, o:o + n] for j in range(k)]
+        want.append(oracle.fedavg(peers, host(w))[0] if r == 0 else oracle.robust(peers, r, b, w=host(w))[0])
+    ops._TABLES.clear()
+    ops.aggregate_slab_rows_(ws, inbox.slab, list(range(k)), offs, rule)
+    for l in range(len(sizes)):
+        assert_bits_equal(host(ws[l]), want[l], nan_equal=True, what=f"{rule} key {l} ({sizes[l]} floats)")
+
+
 def test_slab_rows_path_needs_k16_and_a_round(cuda):
     """Below 16 peers, or below one round of tiles, the slab keeps the
     segment path (the rows entry declines)."""
