@@ -133,13 +133,16 @@ __device__ __forceinline__ void fedavg_elem(const float* const* __restrict__ pee
 // Element-wise over E coordinates per lane at once -- first + stride * j, j
 // < E, those below n -- for views that are only 4-B aligned: every load
 // instruction still reads one contiguous 256 B per wave, and the lane keeps
-// E x 4 loads in flight where one coordinate at a time kept 8 (K = 256 over
+// E x U loads in flight where one coordinate at a time kept 8 (K = 256 over
 // 1.8M coordinates of 8-B aligned rows: 0.18 of HBM peak that way,
 // tools/grid_ab.py).  Each coordinate sums its peers in list order from +0.
+// The VGPR kernels take 8 coordinates x 2 peers per pass: their aligned
+// path's register budget (74 VGPRs) holds, where 16 x 4 took them to 134
+// for the same misaligned rate (0.66 of peak at K = 8, tools/vgpr_ab.py).
 template <int E, bool RECIP>
 __device__ __forceinline__ void fedavg_scalar(const float* const* __restrict__ peers, int K, int64_t n,
                                               int64_t first, int stride, float* w, float* out, float lr) {
-  constexpr int U = 4;
+  constexpr int U = 2;
   bool ok[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) ok[j] = first + static_cast<int64_t>(stride) * j < n;
@@ -198,7 +201,11 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
     }
     return;
   }
-  fedavg_scalar<4 * NV, RECIP>(peers, K, n, tile0 + threadIdx.x, kBlock, w, out, lr);
+  // 8 coordinates per lane per pass (the tile's 4 * NV in passes): the
+  // vector path's register budget holds (64 / 74 VGPRs, occupancy 8 / 6)
+#pragma unroll 1
+  for (int h = 0; h < NV / 2; ++h)
+    fedavg_scalar<8, RECIP>(peers, K, n, tile0 + threadIdx.x + h * 8 * kBlock, kBlock, w, out, lr);
 }
 
 // Flat buffer, one tile per block, tiles tile_base, tile_base + 1, ...  K
