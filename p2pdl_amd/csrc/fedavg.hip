@@ -139,10 +139,9 @@ __device__ __forceinline__ void fedavg_elem(const float* const* __restrict__ pee
 // The VGPR kernels take 8 coordinates x 2 peers per pass: their aligned
 // path's register budget (74 VGPRs) holds, where 16 x 4 took them to 134
 // for the same misaligned rate (0.66 of peak at K = 8, tools/vgpr_ab.py).
-template <int E, bool RECIP>
+template <int E, bool RECIP, int U = 4>
 __device__ __forceinline__ void fedavg_scalar(const float* const* __restrict__ peers, int K, int64_t n,
                                               int64_t first, int stride, float* w, float* out, float lr) {
-  constexpr int U = 2;
   bool ok[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) ok[j] = first + static_cast<int64_t>(stride) * j < n;
@@ -205,7 +204,7 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
   // vector path's register budget holds (64 / 74 VGPRs, occupancy 8 / 6)
 #pragma unroll 1
   for (int h = 0; h < NV / 2; ++h)
-    fedavg_scalar<8, RECIP>(peers, K, n, tile0 + threadIdx.x + h * 8 * kBlock, kBlock, w, out, lr);
+    fedavg_scalar<8, RECIP, 2>(peers, K, n, tile0 + threadIdx.x + h * 8 * kBlock, kBlock, w, out, lr);
 }
 
 // Flat buffer, one tile per block, tiles tile_base, tile_base + 1, ...  K
