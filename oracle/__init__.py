@@ -133,15 +133,18 @@ def fedavg(peers, w=None, lr: float = 0.1, want_out: bool = False, torch_gpu: bo
 
 
 def fedavg_np(peers, w=None, lr: float = 0.1, torch_gpu: bool = False):
-    """numpy restatement (vectorised over coordinates, same op order)."""
-    acc = np.zeros_like(np.asarray(peers[0], dtype=np.float32))
-    for p in peers:
-        acc = acc + np.asarray(p, dtype=np.float32)
-    k = np.float32(len(peers))
-    acc = acc * (np.float32(1.0) / k) if torch_gpu else acc / k
-    if w is None:
-        return None, acc
-    return (np.asarray(w, dtype=np.float32) + np.float32(lr) * acc).astype(np.float32), acc
+    """numpy restatement (vectorised over coordinates, same op order).
+    Overflow to +-inf and inf - inf = NaN are IEEE results here, as in the
+    reference's torch ops (the golden special-value cases): not warned."""
+    with np.errstate(over="ignore", invalid="ignore"):
+        acc = np.zeros_like(np.asarray(peers[0], dtype=np.float32))
+        for p in peers:
+            acc = acc + np.asarray(p, dtype=np.float32)
+        k = np.float32(len(peers))
+        acc = acc * (np.float32(1.0) / k) if torch_gpu else acc / k
+        if w is None:
+            return None, acc
+        return (np.asarray(w, dtype=np.float32) + np.float32(lr) * acc).astype(np.float32), acc
 
 
 # ------------------------------------------------- 16-bit models (a1-a4)
