@@ -702,6 +702,58 @@ def test_pinned_landing_matches_pickle_loads(cuda, proto):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dt", ["float16", "bfloat16"])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_16bit_model_lands_and_aggregates(cuda, dt, pinned, monkeypatch):
+    """A model.half() / bfloat16 node: the 16-bit updates are not
+    slab rows -- land() makes each its own device tensor of the storage's
+    dtype (HalfStorage / BFloat16Storage, bits as sent) -- and
+    aggregate_models over the landed updates == oracle.fedavg16_np (the
+    reference's fp32-op-then-round loop, aggregation.py:15-38, pinned to its
+    own CPU run by tests/golden/fedavg16_golden.npz)."""
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
+    tdt = {"float16": torch.float16, "bfloat16": torch.bfloat16}[dt]
+    k, n = 3, sum(int(np.prod(s)) for _, s in MLP_SHAPES)
+
+    def tensors(bits):
+        out, o = {}, 0
+        for name, s in MLP_SHAPES:
+            m = int(np.prod(s))
+            out[name] = torch.from_numpy(bits[o:o + m].view(np.int16).copy()).view(tdt).reshape(s)
+            o += m
+        return out
+
+    w = oracle.round_16(oracle.synth_np(n, 41, 0xFFFFF, 5e-2), dt)
+    peers = [oracle.round_16(oracle.synth_np(n, 41, p, 1e-2), dt) for p in range(k)]
+    template = {name: t.to(cuda) for name, t in tensors(w).items()}
+    inbox = DeviceInbox(template, k_max=k, device=cuda)
+    assert inbox.row == 0  # no fp32 entry: no slab row
+    ser = [pickle.dumps(tensors(p)) for p in peers]
+    landed = [inbox.land(_pinned(inbox, s) if pinned else s) for s in ser]
+    for got, p in zip(landed, peers):
+        assert list(got) == [name for name, _ in MLP_SHAPES] and not got.slab_keys
+        bits = np.concatenate([got[name].view(torch.int16).cpu().numpy().view(np.uint16).reshape(-1)
+                               for name, _ in MLP_SHAPES])
+        assert np.array_equal(bits, p) and all(got[name].dtype == tdt for name, _ in MLP_SHAPES)
+    model = torch.nn.Module()
+    for name, t in template.items():
+        model.register_parameter(name.replace(".", "__"), torch.nn.Parameter(t.clone(), requires_grad=False))
+    ups = [{name.replace(".", "__"): v for name, v in dict(u).items()} for u in landed]
+    node = types.SimpleNamespace(model=model, trainers_list=[0] * k, addr="a", port=1, neighbors=[],
+                                 received_models=[{"model": u, "sender": j} for j, u in enumerate(ups)])
+    agg.aggregate_models(node)
+    torch.cuda.synchronize()
+    got = np.concatenate([t.detach().view(torch.int16).cpu().numpy().view(np.uint16).reshape(-1)
+                          for t in model.state_dict().values()])
+    want = oracle.fedavg16_np(peers, w, dt)
+    fg, fw = oracle.to_f32_16(got, dt), oracle.to_f32_16(want, dt)
+    assert np.all((got == want) | (np.isnan(fg) & np.isnan(fw))), f"{dt}: {np.count_nonzero(got != want)} differ"
+    assert node.received_models == []
+
+
+@pytest.mark.gpu
 def test_pinned_landing_every_misalignment_and_tail(cuda):
     """Payload offsets mod 4 = 0..3 (a prefix key of 1..4 bytes of name moves
     them) and a tensor ending at the last payload byte of the message."""
