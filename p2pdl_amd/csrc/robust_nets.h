@@ -32,6 +32,33 @@ __device__ __forceinline__ uint64_t unordered_mask(float a, float b) {
   return m;
 }
 
+// a / D correctly rounded (round to nearest even, what `a / float(D)` gives
+// under -fhip-fp32-correctly-rounded-divide-sqrt) in five instructions where
+// the compiler's IEEE division issues eleven: q0 = a * y with y = RN(1/D),
+// the exact residual r = a - q0 * D (one FMA), q1 = q0 + r * y (Markstein's
+// correction: correctly rounded when y is within half an ulp of 1/D, q0
+// within one ulp of a/D and the quotient normal), and v_div_fixup_f32 for
+// the operands the correction cannot take (+-inf: r = inf - inf; NaN).  A
+// subnormal quotient rounds onto the fixed 2^-149 grid, where the
+// correction misses exact and near ties (108,942 of the 2^32 inputs for D =
+// 154, all |a| < 2^-125): a wave with a lane below 2^-118 takes the IEEE division
+// (one compare and a uniform branch).  tools/div_probe.hip checks the whole
+// function against the double quotient for all 2^32 inputs of each divisor.
+template <int D>
+__device__ __forceinline__ float div_const_fast(float a) {
+  constexpr float y = 1.0f / D;
+  const float q0 = __fmul_rn(a, y);
+  const float r = __builtin_fmaf(-q0, static_cast<float>(D), a);
+  return __builtin_amdgcn_div_fixupf(__builtin_fmaf(r, y, q0), static_cast<float>(D), a);
+}
+template <int D>
+__device__ __forceinline__ float div_const(float a) {
+  static_assert(D > 0 && D < (1 << 8), "the 2^-118 bound keeps a / D normal for D < 2^8");
+  if (__builtin_amdgcn_fcmpf(__builtin_fabsf(a), 0x1p-118f, 4 /* ordered less than */) != 0)
+    return a / static_cast<float>(D);
+  return div_const_fast<D>(a);
+}
+
 // Lanes for which any of the N values at(0) .. at(N-1) is NaN.  NaN
 // propagates through v_pk_fma_f32 (a * b + c on float pairs), so each
 // instruction folds four more values into a running pair: the first takes

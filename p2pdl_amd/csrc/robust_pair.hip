@@ -100,6 +100,13 @@ __device__ __forceinline__ void send_run(W32 dst, const T (&m)[kHalf], int lane)
   for (int j = 0; j < N; ++j) dst[j * 64 + lane] = raw(m[FIRST + j]);
 }
 
+// A raw buffer descriptor over a flat float buffer (stride 0, byte offsets;
+// dword 3 as gfx9 parts take it).  Offsets past num_records read 0 / drop
+// the store -- the callers only pass live lanes' offsets.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t flat_rsrc(float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7FFFFFFF, 0x00020000);
+}
+
 __device__ __forceinline__ void block_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -209,7 +216,8 @@ template <int RULE, typename T, bool FLAGS = false, bool PAD = false, int NP = 1
 __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, int h, int lane,
                                            int __attribute__((address_space(3)))* flags = nullptr,
                                            const float* const* P = nullptr, int64_t c0 = 0, uint32_t lane_off = 0,
-                                           int K = 2 * kHalf, const Pads& pd = Pads{}, int pr = 0) {
+                                           int K = 2 * kHalf, const Pads& pd = Pads{}, int pr = 0,
+                                           bool* redo = nullptr) {
   T x[kHalf];
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) x[j] = from_bits<T>(v[j]);
@@ -218,9 +226,15 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   // cone, gen_networks.py NAN_CONE_TAGS) -- where a packed-FMA chain over the
   // loads took 34 instructions per wave
   sort_full<kHalf>(x);
+  // NP == 1: the waves swap their rank-0 outputs instead of flags -- B's is
+  // row 0 of the parity wave 1 hands over anyway, A's goes through the
+  // partial-sum slot (free until barrier 3) -- and both test the same pair
+  // per lane with one compare whose mask the compiler knows is uniform
+  // (llvm.amdgcn.fcmp): 1 VALU where the flag round trip took 13.
+  constexpr bool kSwap0 = FLAGS && NP == 1;
   uint64_t nan = 0;
-  if constexpr (FLAGS) nan = unordered_mask(bits_f(x[0]), bits_f(x[0]));
-  const bool has_nan = FLAGS && uniform(nan != 0);
+  if constexpr (FLAGS && !kSwap0) nan = unordered_mask(bits_f(x[0]), bits_f(x[0]));
+  const bool has_nan = FLAGS && !kSwap0 && uniform(nan != 0);
   pin(x);
   // Batcher's odd-even merge of A (wave 0) and B (wave 1), split by parity:
   // v = merge(A_even, B_even) in wave 0, w = merge(A_odd, B_odd) in wave 1,
@@ -231,20 +245,31 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
   // (the distinct asm after each side's stores keeps LLVM from sinking both
   // into one store sequence fed by moves or selects)
   W32 r0 = reinterpret_cast<W32>(im), r1 = r0 + kHalf / 2 * 64;
+  auto part = (float __attribute__((address_space(3)))*)(im + kHalf / 4 * 64);
   if (h == 0) {
 #pragma unroll
     for (int j = 0; j < kHalf / 2; ++j) r0[j * 64 + lane] = raw(x[2 * j + 1]);
+    if constexpr (kSwap0) part[lane] = bits_f(x[0]);
     asm volatile("; parity hand-off, wave 0" ::: "memory");
   } else {
 #pragma unroll
     for (int j = 0; j < kHalf / 2; ++j) r1[j * 64 + lane] = raw(x[2 * j]);
     asm volatile("; parity hand-off, wave 1" ::: "memory");
   }
-  if constexpr (FLAGS) {
+  if constexpr (FLAGS && !kSwap0) {
     if (lane == 0) flags[2 * pr + h] = has_nan ? 1 : 0;
   }
   block_sync();  // 1: both parities in the image
-  if constexpr (FLAGS) {  // block-wide (same barriers for every pair)
+  // kSwap0: A's rank-0 output (its slot) against B's (row 0 of R1), the same
+  // pair per lane in both waves.  A block holding a NaN finishes the float
+  // path on garbage and the caller re-runs it on the keys (*redo): a call
+  // here, with the sorted halves live on the other path, made LLVM spill ~20
+  // of them around it, and one at each return kept wave 0's sums live across
+  // wave 1's.  Every image read of the float path has completed at barrier
+  // 3, before pair_keys writes.
+  if constexpr (kSwap0)
+    *redo = __builtin_amdgcn_fcmpf(part[lane], __uint_as_float(row_at(r1, 0, lane)), 8 /* unordered */) != 0;
+  if constexpr (FLAGS && !kSwap0) {  // block-wide (same barriers for every pair)
     if (uniform((flags[0] | flags[1] | (NP > 1 ? flags[2] | flags[3] : 0) | (NP > 2 ? flags[4] | flags[5] : 0)) != 0))
       return pair_keys<RULE, PAD>(P, c0, lane_off, im, h, lane, K, pd.lo, pd.m);
   }
@@ -255,7 +280,6 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
     constexpr int IM = kHalf / 2;            // 64: c_127 = min(v_64, w_63), c_128 = max(...)
     constexpr int I1 = kHalf - I0;           // 102: c_204 = max(v_102, w_101)
     constexpr int NX = IM - I0 + 1;          // 39 values cross per wave
-    auto part = (float __attribute__((address_space(3)))*)(im + kHalf / 4 * 64);
     // wave 0 sends v_26..v_64 through R1, wave 1 w_63..w_101 through R0 --
     // each rewrites only the region it read (constant indices: a runtime
     // offset into m would put m in scratch)
@@ -297,7 +321,7 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
       }
       part[lane] = acc;
       block_sync();  // 3: the partial sum of ranks 51..127 in its slot
-      return 0.f;
+      return acc;  // unused (wave 1 stores nothing): no constant to materialise
     }
     T c[2 * (I1 - IM) + 1];  // c_128..c_204
     c[0] = max(m[IM], from_raw<T>(row_at(r0, 0, lane)));
@@ -315,7 +339,7 @@ __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, i
       acc = !PAD || 2 * (IM - I0) + 1 + k < pd.m ? s : acc;  // padded rank b + 77 + k
     }
     if constexpr (PAD) return acc / static_cast<float>(pd.m);
-    return acc / static_cast<float>(2 * kHalf - 2 * b);
+    return div_const<2 * kHalf - 2 * b>(acc);  // = acc / 154.f, bit for bit (robust_nets.h)
   }
 }
 
@@ -390,16 +414,29 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
     N = s.n;
     c0 = (t - s.tile_begin) * (kPairTile * NP) + pr * kPairTile;
   }
-  const int64_t i = c0 + lane;
   // Dead lanes of a ragged tail re-read the last element; with NP > 1 a
   // whole wave pair can lie past the end (it still joins the block's
   // barriers), so its row base is clamped too: 0 <= lane_off < 256 whenever
   // the base carries the tile start.
   // row base offset (SMALL: 0, the whole offset rides per lane; never for
   // PAD, whose pad rows are one tile wide)
-  const int64_t ic = i < N ? i : N - 1;
+  // NARROW (SMALL flat buffers, n <= 2^30): every index a 32-bit byte
+  // offset -- one add and one v_min_u32 per lane, and w / out are read and
+  // written through buffer descriptors at that same offset (no 64-bit
+  // address); the 64-bit form costs ~9 VALU more per wave.
+  constexpr bool NARROW = SMALL && !PAD && !SEGS;
+  const int64_t i = c0 + lane;
   const int64_t cb = SMALL && !PAD ? 0 : (c0 < N ? c0 : N - 1);
-  const uint32_t lane_off = static_cast<uint32_t>(ic - cb) * 4u;
+  uint32_t lane_off;
+  bool live;
+  if constexpr (NARROW) {
+    const uint32_t at = static_cast<uint32_t>(c0) * 4u + lane * 4u, last = static_cast<uint32_t>(N - 1) * 4u;
+    live = at <= last;
+    lane_off = min(at, last);
+  } else {
+    live = i < N;
+    lane_off = static_cast<uint32_t>((live ? i : N - 1) - cb) * 4u;
+  }
   Pads pd;
   if constexpr (PAD) {
     pd.lo = RULE == P2P_RULE_MEDIAN ? (2 * kHalf - 1) / 2 - (K - 1) / 2 : (2 * kHalf * 2) / 10 - trim_b;
@@ -412,10 +449,23 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
   float agg;
   if constexpr (RULE == P2P_RULE_MEDIAN)
     agg = median_pair<fk, true, PAD, NP>(v, im, h, lane, flags, P, cb, lane_off, K, pd, pr);
-  else agg = pair_body<RULE, fk, true, PAD, NP>(v, im, h, lane, flags, P, cb, lane_off, K, pd, pr);
-  if (h == 0 && i < N) {  // wave 0 holds the aggregate
-    if (O) stg(O + i, agg);
-    if (W) stg(W + i, apply_lr(ldg(W + i), lr, agg));
+  else {
+    bool redo = false;  // NP == 1: the NaN test's outcome, acted on here (pair_body)
+    agg = pair_body<RULE, fk, true, PAD, NP>(v, im, h, lane, flags, P, cb, lane_off, K, pd, pr, &redo);
+    if (NP == 1 && redo) agg = pair_keys<RULE, PAD>(P, cb, lane_off, im, h, lane, K, pd.lo, pd.m);
+  }
+  if (h == 0 && live) {  // wave 0 holds the aggregate
+    if constexpr (NARROW) {  // a live lane's offset is its coordinate's
+      if (O) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(agg), flat_rsrc(O), lane_off, 0, 0);
+      if (W) {
+        const auto r = flat_rsrc(W);
+        const float wv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, lane_off, 0, 0));
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(apply_lr(wv, lr, agg)), r, lane_off, 0, 0);
+      }
+    } else {
+      if (O) stg(O + i, agg);
+      if (W) stg(W + i, apply_lr(ldg(W + i), lr, agg));
+    }
   }
 }
 
@@ -429,7 +479,8 @@ __global__ __launch_bounds__(128 * kTrimPairs) __attribute__((amdgpu_waves_per_e
   __shared__ u32x4 img_raw[kImg * kTrimPairs];
   __shared__ int nan_flag[2 * kTrimPairs];
   const int64_t t = tile_id(gx);
-  if (t >= ntiles) return;  // block-uniform
+  // block-uniform; SMALL: fewer than 2^24 tiles, a 32-bit scalar compare
+  if (SMALL ? static_cast<uint32_t>(t) >= static_cast<uint32_t>(ntiles) : t >= ntiles) return;
   const int pr = kTrimPairs == 1 ? 0 : __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 7));
   pair_tile<P2P_RULE_TRIMMED, SEGS, SMALL, PAD, kTrimPairs>(peers, segs, nseg, n, w, out, lr, (Img)img_raw + pr * kImg,
                                                 (int __attribute__((address_space(3)))*)nan_flag, t, K, trim_b);
@@ -445,7 +496,7 @@ robust_median_pair_kernel(const float* const* __restrict__ peers, const Seg* __r
   __shared__ u32x4 img_raw[kImg * kMedianPairs];
   __shared__ int nan_flag[2 * kMedianPairs];
   const int64_t t = tile_id(gx);
-  if (t >= ntiles) return;  // block-uniform
+  if (SMALL ? static_cast<uint32_t>(t) >= static_cast<uint32_t>(ntiles) : t >= ntiles) return;  // block-uniform
   const int pr = kMedianPairs == 1 ? 0 : __builtin_amdgcn_readfirstlane(static_cast<int>(tid_x() >> 7));
   pair_tile<P2P_RULE_MEDIAN, SEGS, SMALL, PAD, kMedianPairs>(peers, segs, nseg, n, w, out, lr,
                                                              (Img)img_raw + pr * kImg,

@@ -861,6 +861,33 @@ def test_robust_structured_extremes(cuda, rule, k):
     assert_bits_equal(host(wt), w_ref, what=f"{rule} apply K={k} structured")
 
 
+@pytest.mark.parametrize("k", [256, 128])
+def test_trimmed_division_edges(cuda, k):
+    """The pair kernel divides by 154 in five instructions (robust_nets.h
+    div_const) and falls back to the IEEE division for |sum| < 2^-118.  Per
+    coordinate, half the peers hold 0 and half v, so the kept ranks sum to
+    an exact multiple of v and the mean is exactly v/2 before rounding:
+    subnormal v with an odd significand is an exact tie (round to even, the
+    fallback), and v near the guard, the normal range, the top of the range
+    (the sum overflows to inf: the fixup) and both zeros cover the rest."""
+    b = ops.trim_count(k)
+    edges = [np.float32(2.0 ** -118), np.float32(np.nextafter(np.float32(2.0 ** -118), np.float32(0))),
+             np.float32(2.0 ** -126), np.float32(1.0), np.float32(3.0e38), np.float32(-3.0e38),
+             np.float32(0.0), np.float32(-0.0), np.float32(np.inf)]
+    rng = np.random.default_rng(k)
+    sub = (rng.integers(1, 1 << 23, 4000) | 1).astype(np.uint32).view(np.float32)  # odd subnormals
+    v = np.concatenate([sub, -sub[:500], np.array(edges, np.float32),
+                        (rng.standard_normal(2000) * 2.0 ** rng.integers(-130, 100, 2000)).astype(np.float32)])
+    n = v.size
+    peers = [np.zeros(n, np.float32) if p % 2 else v.copy() for p in range(k)]
+    w = oracle.synth(n, 5, 0xFFFFF, 5e-2)
+    w_ref, out_ref = oracle.robust(peers, ops.rule_id("trimmed"), b, w=w)
+    wt, out = to_dev(w, cuda), torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.aggregate([to_dev(p, cuda) for p in peers], "trimmed", w=wt, out=out, trim_b=b)
+    assert_bits_equal(host(out), out_ref, what=f"trimmed K={k} division edges")
+    assert_bits_equal(host(wt), w_ref, what=f"trimmed apply K={k} division edges")
+
+
 def test_robust_matches_torch_median(cuda):
     """Independent pin for NaN-free data: torch.median's lower median."""
     k, n = 64, 20000
