@@ -30,9 +30,10 @@
 //
 // Float or key network, per block: each wave sorts its half on the float
 // values themselves (robust_nets.h: same order, same bits as the uint32
-// keys), and the two swap a "my half holds a NaN" flag at the hand-off
-// barrier; a block that finds one re-runs the tile on uint32 total-order
-// keys.  That key path is out of line and re-loads its inputs (pair_keys):
+// keys), and the waves learn at the hand-off barrier whether either half
+// holds a NaN (median: a flag per wave; trimmed: each other's rank-0
+// output, which every NaN reaches); a block that finds one re-runs the tile
+// on uint32 total-order keys.  That key path is out of line and re-loads its inputs (pair_keys):
 // inlined next to the float path, LLVM kept both paths' 128 values live and
 // the kernel took 320-390 VGPRs.
 #include "robust_nets.h"
