@@ -357,6 +357,36 @@ def test_slab_rows_split_path_vs_oracle(cuda, k, rule, monkeypatch):
             assert_bits_equal(host(ws[l]), want[l], what=f"round {rnd} key {l} ({n} floats)")
 
 
+@pytest.mark.parametrize("sizes", [[256 * 8192 - 5], [256 * 8192 - 8192, 8191], [256 * 8192 + 1000]],
+                         ids=["one-round", "one-round-two-keys", "one-round-plus-a-tile"])
+def test_slab_rows_round_edges(cuda, sizes):
+    """The rows kernel at the edges of a CU round: a slab of exactly one
+    round of split tiles, one round ending in a second key, and one round
+    plus one tile (the last tile mostly padding), bit-exact against the
+    oracle."""
+    from p2pdl_amd.node.inbox import DeviceInbox
+
+    k = 16
+    template = {f"k{i}": torch.zeros(n, device=cuda) for i, n in enumerate(sizes)}
+    inbox = DeviceInbox(template, k_max=k, device=cuda)
+    offs = [inbox.layout[f"k{i}"][0] for i in range(len(sizes))]
+    assert all(o % 1024 == 0 for o in offs)
+    for j in range(k):
+        ops.fill_synthetic_(inbox.slab[j], 0x7050, j, 1e-2)
+    ws = []
+    for i, n in enumerate(sizes):
+        w = torch.empty(n, dtype=torch.float32, device=cuda)
+        ops.fill_synthetic_(w, 0x7051, i, 5e-2)
+        ws.append(w)
+    rows_host = inbox.slab[:k].cpu().numpy()
+    want = [oracle.fedavg([rows_host[j, o:o + n] for j in range(k)], host(w))[0] for o, n, w in zip(offs, sizes, ws)]
+    ops._TABLES.clear()
+    entry = ops.aggregate_slab_rows_(ws, inbox.slab, list(range(k)), offs, "fedavg")
+    assert entry is not None and entry[5][0] == "rows"
+    for l, n in enumerate(sizes):
+        assert_bits_equal(host(ws[l]), want[l], what=f"key {l} ({n} floats)")
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_slab_rows_random_layouts(cuda, seed):
     """Random state_dict shapes (1..1100 floats and a few large tensors, random
