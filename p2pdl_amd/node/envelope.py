@@ -99,20 +99,36 @@ class _Tensor:
 
 class _Layout:
     """One pinned buffer of legacy blobs for a fixed list of fp32 sizes and
-    storage locations."""
+    storage locations.  The blobs the pickler copies (below _INLINE_MAX)
+    come first, then the large ones; every payload starts 256-B aligned
+    (the slots are separate views, so the gaps never reach the pickle).
+    For a model on one GPU a device image of the buffer (headers written
+    once) takes the weights by one gather kernel, and two DMAs bring it
+    over: the small blobs' region, then the rest."""
 
-    def __init__(self, numels, locations, pin: bool):
+    def __init__(self, numels, locations, pin: bool, device=None):
         heads = [legacy_storage_header(n, str(i), loc) for i, (n, loc) in enumerate(zip(numels, locations))]
-        self.spans = []  # (blob start, payload start, blob end) per tensor
-        off = 0
-        for h, n in zip(heads, numels):
-            self.spans.append((off, off + len(h), off + len(h) + 4 * n))
-            off += len(h) + 4 * n
+        order = sorted(range(len(heads)), key=lambda i: len(heads[i]) + 4 * numels[i] >= _INLINE_MAX)
+        self.spans = [None] * len(heads)  # (blob start, payload start, blob end) per tensor
+        off = self.inline_end = 0
+        for i in order:
+            a = -(-(off + len(heads[i])) // 256) * 256 - len(heads[i])
+            self.spans[i] = (a, a + len(heads[i]), a + len(heads[i]) + 4 * numels[i])
+            off = self.spans[i][2]
+            if len(heads[i]) + 4 * numels[i] < _INLINE_MAX:
+                self.inline_end = off
         self.buf = torch.empty(max(off, 1), dtype=torch.uint8, pin_memory=pin)  # DMA target for GPU weights
         arr = self.buf.numpy()
+        arr[:] = 0
         for h, (a, p, _) in zip(heads, self.spans):
             arr[a:p] = np.frombuffer(h, dtype=np.uint8)
         self.mv = memoryview(arr).toreadonly()
+        self.dev = None
+        if device is not None:
+            self.dev = torch.empty_like(self.buf, device=device)
+            self.dev.copy_(self.buf)  # the headers, once
+            torch.cuda.current_stream(device).synchronize()
+        self.gather = None  # (source pointers, device table, base, span, segments, tiles)
 
 
 _LAYOUTS = {}
@@ -139,11 +155,21 @@ def _layout_for(purpose, fast):
     sig = (purpose, locs, tuple(t.numel() for _, t in fast))
     lay = _LAYOUTS.get(sig)
     if lay is None:
-        lay = _Layout(sig[2], locs, any(t.is_cuda for _, t in fast))
+        devs = {t.device for _, t in fast}
+        one_gpu = len(devs) == 1 and next(iter(devs)).type == "cuda"
+        lay = _Layout(sig[2], locs, any(t.is_cuda for _, t in fast), next(iter(devs)) if one_gpu else None)
         for old in [k for k in _LAYOUTS if k[0] == purpose]:
             del _LAYOUTS[old]  # one model per purpose: keep the latest layout only
         _LAYOUTS[sig] = lay
     return lay
+
+
+# A blob below this size is copied into the pickler's frame while it
+# pickles (CPython's _pickle hands a payload of FRAME_SIZE_TARGET = 64 KiB or
+# more to the writer as the object itself, uncopied): its DMA must have
+# landed before the pickler runs, a larger one only before the parts are
+# read.  1 MiB leaves a margin; tests/test_envelope.py pins the behaviour.
+_INLINE_MAX = 1 << 20
 
 
 def envelope_parts(state, addr, port):
@@ -155,8 +181,10 @@ def envelope_parts(state, addr, port):
     the parts (the next call reuses the slots).  Other tensors pickle as
     torch pickles them, from the host."""
     out = _Parts()
-    pickle.Pickler(out, protocol=5).dump({"type": "global_model_update", "model": _placeholders(state),
+    model, settle = _fill(state)
+    pickle.Pickler(out, protocol=5).dump({"type": "global_model_update", "model": model,
                                           "addr": addr, "port": port})
+    settle()  # the large blobs' DMAs ran beside the pickler
     return out.parts
 
 
@@ -168,24 +196,61 @@ def dumps_state(state) -> bytes:
     and the inbox's parser read it as they read torch's pickle."""
     with LOCK:
         out = _Parts()
-        pickle.Pickler(out, protocol=5).dump(_placeholders(state, purpose="update"))
+        model, settle = _fill(state, purpose="update")
+        pickle.Pickler(out, protocol=5).dump(model)
+        settle()
         return b"".join(out.parts)
 
 
 def _placeholders(state, purpose="global"):
     """The state_dict with each contiguous fp32 tensor replaced by a _Tensor
     over its freshly filled pinned blob slot (caller holds LOCK)."""
+    model, settle = _fill(state, purpose)
+    settle()
+    return model
+
+
+def _fill(state, purpose="global"):
+    """_placeholders without waiting for the large slots: the DMAs of blobs
+    the pickler copies (below _INLINE_MAX) are issued first and waited for
+    here; the large ones after them, waited for by ``settle()`` -- so the
+    pickler runs while they stream (caller holds LOCK)."""
     items = list(state.items())
     fast = [(k, t) for k, t in items if t.dtype == torch.float32 and t.is_contiguous()]
     model = collections.OrderedDict() if isinstance(state, collections.OrderedDict) else type(state)()
     slots = {}
+    devices = []
     if fast:
         lay = _layout_for(purpose, fast)
-        for (k, t), (a, p, e) in zip(fast, lay.spans):
-            if t.numel():
-                lay.buf[p:e].copy_(t.detach().reshape(-1).view(torch.uint8), non_blocking=t.is_cuda)
-            slots[k] = (t, lay.mv[a:e])
-        for d in {t.device for _, t in fast if t.is_cuda}:
+        spans = list(zip(fast, lay.spans))
+        devices = list({t.device for _, t in fast if t.is_cuda})
+        inline_done = []
+        if lay.dev is not None:  # one gather kernel, two DMAs
+            with torch.cuda.device(lay.dev.device):
+                _gather(lay, fast)
+                if lay.inline_end:
+                    lay.buf[:lay.inline_end].copy_(lay.dev[:lay.inline_end], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(lay.dev.device))
+                inline_done.append(ev)
+                if lay.inline_end < lay.buf.numel():
+                    lay.buf[lay.inline_end:].copy_(lay.dev[lay.inline_end:], non_blocking=True)
+        else:
+            for large in (False, True):
+                for (k, t), (a, p, e) in spans:
+                    if (e - a >= _INLINE_MAX) == large and t.numel():
+                        lay.buf[p:e].copy_(t.detach().reshape(-1).view(torch.uint8), non_blocking=t.is_cuda)
+                if not large:
+                    for d in devices:
+                        ev = torch.cuda.Event()
+                        ev.record(torch.cuda.current_stream(d))
+                        inline_done.append(ev)
+        for ev in inline_done:
+            ev.synchronize()
+        slots = {k: (t, lay.mv[a:e]) for (k, t), (a, _, e) in spans}
+
+    def settle():
+        for d in devices:
             torch.cuda.current_stream(d).synchronize()
     for k, t in items:
         if k in slots:
@@ -193,7 +258,44 @@ def _placeholders(state, purpose="global"):
             model[k] = _Tensor(_Blob(mv), tuple(src.shape), tuple(src.stride()))
         else:
             model[k] = t.detach()  # pickled by torch, as the reference pickles it
-    return model
+    return model, settle
+
+
+_LAND_TILE = 4096  # == P2P_LAND_TILE
+_LAND_SEG = np.dtype([("src_off", "<u8"), ("dst", "<u8"), ("n", "<i8"), ("tile_begin", "<i8")])
+
+
+def _gather(lay, fast):
+    """Every fp32 tensor into its payload slot of the device image, one
+    p2p_land_segments_f32 launch (K5's landing kernel as a gather: the
+    sources are offsets from the lowest tensor address).  The segment table
+    is built and uploaded when the tensors' addresses change (a model's
+    parameters keep theirs across rounds)."""
+    from .. import _native as N
+    from .. import ops
+
+    ptrs = tuple(t.data_ptr() for _, t in fast)
+    if lay.gather is None or lay.gather[0] != ptrs:
+        live = [(t.data_ptr(), t.numel(), p) for (_, t), (_, p, _) in zip(fast, lay.spans) if t.numel()]
+        table = None
+        base = span = ntiles = 0
+        if live:
+            base = min(a for a, _, _ in live)
+            span = max(a + 4 * n for a, n, _ in live) - base
+            tab = np.zeros(len(live), dtype=_LAND_SEG)
+            tab["src_off"] = [a - base for a, _, _ in live]
+            tab["dst"] = [lay.dev.data_ptr() + p for _, _, p in live]
+            n_arr = np.array([n for _, n, _ in live], dtype=np.int64)
+            tab["n"] = n_arr
+            t_arr = -(-n_arr // _LAND_TILE)
+            tab["tile_begin"][1:] = np.cumsum(t_arr)[:-1]
+            ntiles = int(t_arr.sum())
+            table = torch.from_numpy(tab.view(np.uint8).copy()).to(lay.dev.device)
+        lay.gather = (ptrs, table, base, span, len(live), ntiles)
+    _, table, base, span, nseg, ntiles = lay.gather
+    if nseg:
+        N.check(N.lib().p2p_land_segments_f32(base, span, table.data_ptr(), nseg, ntiles,
+                                              N.stream_handle(lay.dev.device)), "p2p_land_segments_f32")
 
 
 def global_model_envelope(state, addr, port) -> bytes:

@@ -102,6 +102,25 @@ def test_envelope_parts_alias_the_slots_and_join_to_the_envelope():
     assert joined == E.global_model_envelope(sd, "h", 1)
 
 
+def test_pickler_hands_large_blobs_over_uncopied():
+    """envelope._fill waits only for the DMAs of blobs below _INLINE_MAX
+    before pickling: CPython's pickler copies smaller in-band payloads into
+    its frame (it reads them then) and hands larger ones to the writer as
+    the object itself (read only when the parts are).  Pin both halves: a
+    blob of _INLINE_MAX bytes written after pickling shows in the parts, and
+    the pickler's own cut-off lies below _INLINE_MAX."""
+    def aliased(size):
+        buf = bytearray(size)
+        out = E._Parts()
+        pickle.Pickler(out, protocol=5).dump({"blob": E._Blob(memoryview(buf).toreadonly())})
+        buf[:4] = b"late"  # the DMA landing after the pickler ran
+        return b"late" in b"".join(out.parts)
+
+    assert aliased(E._INLINE_MAX) and not aliased(1024)
+    cut = next(s for s in (1 << k for k in range(10, 21)) if aliased(s))
+    assert cut <= E._INLINE_MAX // 4, cut  # 64 KiB on CPython 3.8-3.13
+
+
 def test_envelope_passes_the_restricted_parser():
     """A peer running p2pdl_amd's receive path parses the global model with
     the restricted machine (no unpickler on peer bytes): same payloads."""
@@ -147,3 +166,25 @@ def test_envelope_from_gpu_model(cuda):
         with torch.no_grad():
             for p in net.parameters():
                 p.add_(1.0)  # new values, same layout
+
+
+@pytest.mark.gpu
+def test_envelope_large_gpu_tensors_settle_before_the_parts_are_read(cuda):
+    """Blobs of _INLINE_MAX bytes or more are DMA'd while the pickler runs
+    (envelope._fill) and waited for before the parts are handed out: every
+    call's envelope and update carry the values of that call, bit for bit,
+    with each round's new values written by a kernel just before it."""
+    sd = collections.OrderedDict([("conv.weight", torch.empty(512, 512, 3, 3, device=cuda)),
+                                  ("bn.weight", torch.empty(512, device=cuda)),
+                                  ("fc.weight", torch.empty(1000, 512, device=cuda)),
+                                  ("small", torch.empty(70_000, device=cuda))])
+    for rnd in range(3):
+        with torch.no_grad():
+            for i, t in enumerate(sd.values()):
+                t.copy_(torch.arange(t.numel(), device=cuda, dtype=torch.float32).view_as(t) * (rnd + 1) + i)
+        with E.LOCK:
+            joined = b"".join(E.envelope_parts(sd, "h", 1))
+        got = pickle.loads(joined)["model"]
+        upd = pickle.loads(E.dumps_state(sd))
+        for k, v in sd.items():
+            assert torch.equal(got[k], v) and torch.equal(upd[k], v), (rnd, k)
