@@ -202,9 +202,13 @@ __device__ __forceinline__ void fedavg_tile(const float* const* __restrict__ pee
   }
   // 8 coordinates per lane per pass (the tile's 4 * NV in passes): the
   // vector path's register budget holds (64 / 74 VGPRs, occupancy 8 / 6)
+  if constexpr (NV == 1) {
+    fedavg_scalar<4, RECIP, 2>(peers, K, n, tile0 + threadIdx.x, kBlock, w, out, lr);
+  } else {
 #pragma unroll 1
-  for (int h = 0; h < NV / 2; ++h)
-    fedavg_scalar<8, RECIP, 2>(peers, K, n, tile0 + threadIdx.x + h * 8 * kBlock, kBlock, w, out, lr);
+    for (int h = 0; h < NV / 2; ++h)
+      fedavg_scalar<8, RECIP, 2>(peers, K, n, tile0 + threadIdx.x + h * 8 * kBlock, kBlock, w, out, lr);
+  }
 }
 
 // Flat buffer, one tile per block, tiles tile_base, tile_base + 1, ...  K
@@ -441,13 +445,20 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
 }
 
 // Whole state_dict: one tile per block, segment found by binary search.
-template <bool RECIP>
+// QUARTERS: a table of fewer tiles than the chip has CUs (the reference's
+// MNIST MLP: 134) runs four blocks per tile, each a quarter (one float4 per
+// lane per peer), so the launch covers the chip; the table is the same.
+template <bool RECIP, bool QUARTERS = false>
 __global__ __launch_bounds__(kBlock) void fedavg_segments_kernel(const Seg* __restrict__ segs,
                                                                  int nseg, int K, float lr) {
-  const int64_t t = blockIdx.x;
+  const int64_t t = QUARTERS ? blockIdx.x >> 2 : blockIdx.x;
   const Seg s = load_segment(segs, nseg, t);
   const bool aligned = all_aligned16(s.peers, K, s.w, s.out);
-  fedavg_tile<kNV, RECIP>(s.peers, K, s.n, (t - s.tile_begin) * kTile, s.w, s.out, lr, aligned);
+  if constexpr (QUARTERS)
+    fedavg_tile<1, RECIP>(s.peers, K, s.n, (t - s.tile_begin) * kTile + (blockIdx.x & 3) * tile_of<1>(), s.w, s.out,
+                          lr, aligned);
+  else
+    fedavg_tile<kNV, RECIP>(s.peers, K, s.n, (t - s.tile_begin) * kTile, s.w, s.out, lr, aligned);
 }
 
 __global__ __launch_bounds__(kBlock) void apply_kernel(float* w, const float* agg, float lr,
@@ -622,13 +633,17 @@ extern "C" P2P_INTERNAL int32_t p2p_fedavg_segments_f32(const p2p_segment_t* seg
                                            p2p_stream_t stream, int32_t recip) {
   if (!segs || nseg < 1 || k < 1 || total_tiles < 0) return P2P_ERR_INVALID;
   if (total_tiles == 0) return P2P_OK;
+  static_assert(kTile == 4 * tile_of<1>(), "four quarters per tile");
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  if (total_tiles < device_cus()) {
+    const dim3 grid(static_cast<unsigned>(4 * total_tiles));
+    if (recip) hipLaunchKernelGGL((fedavg_segments_kernel<true, true>), grid, dim3(kBlock), 0, st, segs, nseg, k, lr);
+    else hipLaunchKernelGGL((fedavg_segments_kernel<false, true>), grid, dim3(kBlock), 0, st, segs, nseg, k, lr);
+    return launch_status();
+  }
   const dim3 grid(static_cast<unsigned>(total_tiles));
-  if (recip)
-    hipLaunchKernelGGL(fedavg_segments_kernel<true>, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), segs,
-                       nseg, k, lr);
-  else
-    hipLaunchKernelGGL(fedavg_segments_kernel<false>, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), segs,
-                       nseg, k, lr);
+  if (recip) hipLaunchKernelGGL(fedavg_segments_kernel<true>, grid, dim3(kBlock), 0, st, segs, nseg, k, lr);
+  else hipLaunchKernelGGL(fedavg_segments_kernel<false>, grid, dim3(kBlock), 0, st, segs, nseg, k, lr);
   return launch_status();
 }
 
