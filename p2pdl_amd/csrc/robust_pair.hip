@@ -210,9 +210,11 @@ __device__ __forceinline__ float median_pair(const uint32_t (&v)[kHalf], Img im,
   return val(two_set_median<Q>(x, y));
 }
 
-// FLAGS (float path): the two waves swap "my half holds a NaN" at barrier 1,
-// beside the hand-off; a block that finds one re-runs the tile on the key
-// network (pair_keys) -- the float sort of a NaN half is discarded.
+// FLAGS (float path): the two waves learn at barrier 1, beside the hand-off,
+// whether either half holds a NaN; a block that finds one re-runs the tile
+// on the key network (pair_keys) -- the float sort of a NaN half is
+// discarded.  NP == 1 (the product's trimmed kernels) reports it through
+// *redo and the caller re-runs after the float path; NP > 1 calls here.
 template <int RULE, typename T, bool FLAGS = false, bool PAD = false, int NP = 1>
 __device__ __forceinline__ float pair_body(const uint32_t (&v)[kHalf], Img im, int h, int lane,
                                            int __attribute__((address_space(3)))* flags = nullptr,
