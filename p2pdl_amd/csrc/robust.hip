@@ -82,7 +82,7 @@ __device__ __forceinline__ float special_floats(const uint32_t (&v)[KP], uint64_
     }
 #pragma unroll
     for (int j = b; j < KP - b; ++j) acc = __fadd_rn(acc, x[j].x);
-    return acc / static_cast<float>(KP - 2 * b);
+    return div_const<KP - 2 * b>(acc);  // = acc / float(KP - 2b), bit for bit (robust_nets.h)
   }
 }
 
@@ -188,7 +188,7 @@ __device__ __forceinline__ float robust_coord(const float* const* __restrict__ p
       constexpr int b = (KP * 2) / 10;  // floor(0.2 KP) for KP in {64,128,256}
 #pragma unroll
       for (int j = b; j < KP - b; ++j) acc = __fadd_rn(acc, __uint_as_float(key2f(v[j])));
-      return acc / static_cast<float>(KP - 2 * b);
+      return div_const<KP - 2 * b>(acc);
     } else {
       const int hi = K - trim_b;
 #pragma unroll

@@ -41,7 +41,7 @@ __device__ __forceinline__ uint64_t unordered_mask(float a, float b) {
 // the operands the correction cannot take (+-inf: r = inf - inf; NaN).  A
 // subnormal quotient rounds onto the fixed 2^-149 grid, where the
 // correction misses exact and near ties (108,942 of the 2^32 inputs for D =
-// 154, all |a| < 2^-125): a wave with a lane below 2^-118 takes the IEEE division
+// 154, all |a| < 2^-125; below 2^-124 for 40): a wave with a lane below 2^-118 takes the IEEE division
 // (one compare and a uniform branch).  tools/div_probe.hip checks the whole
 // function against the double quotient for all 2^32 inputs of each divisor.
 template <int D>

@@ -79,5 +79,6 @@ static void run() {
 int main() {
   run<154>();  // trimmed mean at K = 256, b = 51
   run<78>();   // K = 128, b = 25
+  run<40>();   // K = 64, b = 12
   return 0;
 }
