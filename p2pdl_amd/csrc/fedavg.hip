@@ -530,6 +530,23 @@ static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, 
     }
   }
   static_assert(kSTile % kTile == 0, "split tiles are whole VGPR tiles");
+  // A remainder (or a whole buffer) of fewer 4096-float tiles than CUs --
+  // the split kernel's rest: ~231 per cfg3 plane -- runs 1024-float tiles,
+  // four times the blocks, so every CU streams.
+#ifndef P2P_FLAT_QUARTERS
+#define P2P_FLAT_QUARTERS 1
+#endif
+  if (P2P_FLAT_QUARTERS && ceil_div(n - done, kTile) < device_cus()) {
+    const int64_t qbase = done / tile_of<1>();
+    const dim3 qgrid(grid_for_tiles(ceil_div(n - done, tile_of<1>())));
+    if (recip)
+      hipLaunchKernelGGL((fedavg_flat_kernel<1, true>), qgrid, dim3(kBlock), 0, stream, peers, K, k_dev, n, w, out, lr,
+                         qbase);
+    else
+      hipLaunchKernelGGL((fedavg_flat_kernel<1, false>), qgrid, dim3(kBlock), 0, stream, peers, K, k_dev, n, w, out,
+                         lr, qbase);
+    return;
+  }
   const int64_t tile_base = done / kTile;
   const dim3 grid(grid_for_tiles(ceil_div(n - done, kTile)));
   if (recip)
