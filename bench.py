@@ -246,19 +246,29 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
     # the product's memory-sharded layout (sharded.PeerPlanes): chunk-major
     # planes of K rows spanning <= 16 GB each, at least the all-gather
     # pipeline's chunks at N > 1
-    S = sharded.plane_count(K, n, at_least=chunks if world > 1 else 1)
-    C = n // S
+    if rule == "fedavg" and world == 1 and K >= 16:
+        # one rank: planes of whole split-kernel CU rounds, one short last
+        # plane (sharded.round_plane_sizes; +1.3-1.7% on cfg3, same box)
+        sizes = sharded.round_plane_sizes(
+            K, n, torch.cuda.get_device_properties(dev).multi_processor_count * ops.SPLIT_TILE)
+    else:  # N > 1: equal chunks, the all-gather pipeline's round robin
+        S = sharded.plane_count(K, n, at_least=chunks if world > 1 else 1)
+        sizes = [n // S] * S
+    # C = the longest (first) plane: the synthetic chunk map's chunk, so plane
+    # s holds global coordinates [s*C*N + rank*C, ...) -- a shorter last plane
+    # is the head of its chunk
+    S, C = len(sizes), sizes[0]
     free, _ = torch.cuda.mem_get_info(dev)
     need = (K + 2 + world) * n * 4
     if need > free * 0.97:
         raise SystemExit(f"{name}: needs {need/1e9:.1f} GB, {free/1e9:.1f} GB free")
     log(f"[rank {rank}] {name}: generating {K} x {n:,} fp32 peer data ({K*n*4/1e9:.1f} GB) "
-        f"as {S} plane(s) of {K} x {C:,}")
-    planes, w = sharded.PeerPlanes(K, S, C, dev), pitched_slab(1, S, C, dev)[0]
+        f"as {plane_desc(K, sizes)}")
+    planes, w = sharded.PeerPlanes(K, S, C, dev, sizes=sizes), pitched_slab(1, S, C, dev)[0]
     for s in range(S):  # local chunk s is global chunk s*N + rank
         for p in range(K):
             ops.fill_synthetic_(planes.row(s, p), seed, p, UPD_SCALE, C, world, rank + s * world)
-        ops.fill_synthetic_(w[s, :C], seed, W_PEER, W_SCALE, C, world, rank + s * world)
+        ops.fill_synthetic_(w[s, :sizes[s]], seed, W_PEER, W_SCALE, C, world, rank + s * world)
     w_full = torch.empty(n * world, dtype=torch.float32, device=dev) if world > 1 else None
     tables = planes.tables
     torch.cuda.synchronize()
@@ -268,7 +278,7 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
 
     gath = []
 
-    wviews = [w[s, :C] for s in range(S)]
+    wviews = [w[s, :sizes[s]] for s in range(S)]
 
     def step(record=False):
         # the product's round (sharded.PeerPlanes.aggregate_gather_): every
@@ -300,8 +310,9 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
             bad = [g for g in range(world)
                    if not bits_equal((w_full[g * C:g * C + m] if world > 1 else w[0, :m]).cpu().numpy(),
                                      oracle_expect(rule, K, m, seed, C, world, g))]
-            if S > 1 and not bits_equal(w[S - 1, :m].cpu().numpy(),  # rank 0's last plane too
-                                        oracle_expect(rule, K, m, seed, C, world, (S - 1) * world)):
+            ml = min(m, sizes[-1])
+            if S > 1 and not bits_equal(w[S - 1, :ml].cpu().numpy(),  # rank 0's last plane too
+                                        oracle_expect(rule, K, ml, seed, C, world, (S - 1) * world)):
                 bad.append(f"rank 0 plane {S - 1}")
             log(f"[rank 0] {name}: spot check vs oracle ({m} coords x {world} rank chunk(s)"
                 f"{' + the last plane' if S > 1 else ''}): {'bit-exact' if not bad else f'MISMATCH on {bad}'}")
@@ -341,7 +352,7 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
         # (coordinate-wise, so chunk by chunk is the same computation)
         def reference_step():
             for s in range(S):
-                ws = w[s, :C]
+                ws = w[s, :sizes[s]]
                 acc = torch.zeros_like(ws)  # :15
                 for p in range(K):  # :25-28
                     acc += planes.row(s, p)
@@ -384,15 +395,23 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
                                + (" (cfg3 per-GPU tile; N=8 -> the 1B-coordinate job)" if name == "cfg3" else ""),
                    "rule": rule, "peers": K, "coords_per_gpu": n, "coords_total": n * world,
                    "parallelism": parallelism(c),
-                   "layout": f"{S} chunk-major plane(s) of {K} x {C:,} (sharded.PeerPlanes), one launch per plane",
+                   "layout": f"{plane_desc(K, sizes)} (sharded.PeerPlanes), one launch per plane",
                    "pct_hbm_peak_step": round(4 * n * (K + 2) / step_s / 1e9 / HBM_PEAK_GBS, 4)}
                   | ({"per_rank": per_rank, "chunks_per_rank": S, "chunk_coords": C} | dist_info() if per_rank else {})
                   | ({"reference_on_gpu_ms_per_step": round(ref_s * 1e3, 3),
                       "speedup_vs_reference_on_gpu": round(ref_s / step_s, 2)} if ref_s else {}),
-        "roofline": roofline(4 * C * (K + 2), kern_ms, traffic_for(name, C, K)),
+        # per launch: the mean plane (= every plane when they are equal);
+        # Σ bytes / Σ kernel time either way
+        "roofline": roofline(4 * n * (K + 2) / S, kern_ms, traffic_for(name, n / S, K)),
         "cpu_baseline": cpu,
     }
     return rec, step_s
+
+
+def plane_desc(K, sizes) -> str:
+    runs = [(c, sizes.count(c)) for c in dict.fromkeys(sizes)]
+    return (f"{len(sizes)} chunk-major plane(s): "
+            + " + ".join(f"{cnt} x [{K} x {c:,}]" for c, cnt in runs))
 
 
 # ------------------------------------------------------------------ cfg3 full job

@@ -55,6 +55,21 @@ def plane_count(k: int, n: int, at_least: int = 1) -> int:
     raise ValueError(f"no chunk count in [{s0}, {64 * s0}] divides {n} coordinates evenly")
 
 
+def round_plane_sizes(k: int, n: int, round_coords: int) -> list[int]:
+    """Plane lengths for n coordinates of k rows, one launch each: planes of
+    whole split-kernel CU rounds (``round_coords`` = CUs x 8192 floats), as
+    many rounds as fit PLANE_BYTES, and one short last plane with the only
+    remainder -- where ``plane_count``'s equal planes leave every plane a
+    partial round for the VGPR kernel.  Same box, interleaved, over one
+    buffer (tools/grid_ab.py wholeplanes, profiles/r05/wholeplanes): the cfg3
+    tile (256 x 125M) as 7 x 16,777,216 + 7,559,488 runs 19.20-19.69 ms
+    against 19.51-19.94 for 8 x 15,625,000, +1.3-1.7% in each of three passes."""
+    m = max(1, PLANE_BYTES // (4 * k * round_coords)) * round_coords
+    if n <= m:
+        return [n]
+    return [m] * (n // m) + ([n % m] if n % m else [])
+
+
 class PeerPlanes:
     """The memory-sharded receive layout of one rank: S chunks of C
     coordinates from each of K peers, CHUNK-MAJOR -- plane s holds chunk s of
@@ -64,10 +79,19 @@ class PeerPlanes:
     ``tables[s]`` the device pointer table of plane s, ``reduce_(s, w, ...)``
     the rule over it (the HIP kernels; no fallback) and ``aggregate_gather_``
     one whole round: every plane, each plane's all-gather beside the next
-    plane's reduction."""
+    plane's reduction.  ``sizes`` gives planes of unequal lengths (the last
+    may be shorter, ``round_plane_sizes``): plane s holds ``sizes[s]``
+    coordinates at offset ``offsets[s]``; ``chunk`` is then the longest."""
 
-    def __init__(self, k: int, chunks: int, chunk: int, device):
+    def __init__(self, k: int, chunks: int, chunk: int, device, sizes: Sequence[int] | None = None):
+        if sizes is not None:
+            sizes = [int(c) for c in sizes]
+            if not sizes or min(sizes) <= 0:
+                raise ValueError(f"plane sizes must be positive, got {sizes}")
+            chunks, chunk = len(sizes), max(sizes)
         self.k, self.chunks, self.chunk = int(k), int(chunks), int(chunk)
+        self.sizes = sizes or [self.chunk] * self.chunks
+        self.offsets = [sum(self.sizes[:s]) for s in range(self.chunks)]
         self.pitch = -(-self.chunk // ROW_ALIGN) * ROW_ALIGN
         self.data = torch.empty((self.chunks, self.k, self.pitch), dtype=torch.float32, device=device)
         self._tables = None
@@ -82,7 +106,7 @@ class PeerPlanes:
         return self._tables
 
     def row(self, s: int, p: int) -> torch.Tensor:
-        return self.data[s, p, :self.chunk]
+        return self.data[s, p, :self.sizes[s]]
 
     def reduce_(self, s: int, w: torch.Tensor, rule="fedavg", *, lr: float = 0.1,
                 trim_frac: float = 0.2) -> None:
@@ -97,10 +121,11 @@ class PeerPlanes:
         chunk s of w -- global chunk s*G + rank (ChunkPlan's round robin) --
         updated in place.  With ``w_full`` and an initialised process group,
         round s's all-gather writes every rank's chunk s to the contiguous
-        w_full[s*G*C, (s+1)*G*C): on ``comm`` (a second stream) beside plane
+        w_full[o*G, (o+C)*G) (o, C = offsets[s], sizes[s]; equal planes:
+        [s*G*C, (s+1)*G*C)): on ``comm`` (a second stream) beside plane
         s+1's reduction, the compute stream waiting for the last one; without
         ``comm``, in line.  Without a process group (one rank), chunk s is
-        copied to w_full[s*C, (s+1)*C).  ``hook(s, phase, stream)`` runs at "reduce0" /
+        copied to w_full[o, o+C).  ``hook(s, phase, stream)`` runs at "reduce0" /
         "reduce1" / "gather0" / "gather1" on the stream of that step (timing
         events); ``reduce(planes, s, w, rule, lr, trim_frac)`` replaces the HIP
         reduction (the CPU gloo tests)."""
@@ -108,9 +133,9 @@ class PeerPlanes:
             raise ValueError(f"{len(ws)} w chunks for {self.chunks} planes")
         gather = w_full is not None and dist.is_initialized()
         G = dist.get_world_size(group) if gather else 1
-        C = self.chunk
-        if w_full is not None and w_full.numel() < self.chunks * G * C:
-            raise ValueError(f"w_full has {w_full.numel()} elements, the round needs {self.chunks * G * C}")
+        total = sum(self.sizes)
+        if w_full is not None and w_full.numel() < total * G:
+            raise ValueError(f"w_full has {w_full.numel()} elements, the round needs {total * G}")
         comp = torch.cuda.current_stream(self.data.device) if self.data.is_cuda else None
         for s in range(self.chunks):
             if hook:
@@ -121,11 +146,12 @@ class PeerPlanes:
                 reduce(self, s, ws[s], rule, lr, trim_frac)
             if hook:
                 hook(s, "reduce1", comp)
+            o, C = self.offsets[s], self.sizes[s]
             if not gather:
                 if w_full is not None:
-                    w_full[s * C:(s + 1) * C].copy_(ws[s])
+                    w_full[o:o + C].copy_(ws[s])
                 continue
-            out = w_full[s * G * C:(s + 1) * G * C]
+            out = w_full[o * G:(o + C) * G]
             if comm is not None:
                 ev = torch.cuda.Event()
                 ev.record(comp)

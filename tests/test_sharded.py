@@ -76,6 +76,30 @@ def test_peer_planes_layout_and_reduce(cuda):
         planes.reduce_(0, torch.zeros(chunk + 1, device=cuda))
 
 
+@pytest.mark.gpu
+def test_peer_planes_whole_rounds_on_the_split_kernel(cuda):
+    """round_plane_sizes' layout through the HIP path: planes of whole CU
+    rounds (the split kernel alone) and a short last plane (split rounds + the
+    VGPR remainder), one aggregate_gather_ into w_full, bit-exact against the
+    oracle; K = 16, the split kernel's smallest K."""
+    k, seed = 16, 0x91B
+    R = torch.cuda.get_device_properties(cuda).multi_processor_count * 8192
+    sizes = [2 * R, 2 * R, R + 3 * 8192 + 1000]
+    n = sum(sizes)
+    planes = sharded.PeerPlanes(k, 0, 0, cuda, sizes=sizes)
+    peers = [oracle.synth(n, seed, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, seed, 0xFFFFF, 5e-2)
+    ws = []
+    for s, (o, c) in enumerate(zip(planes.offsets, planes.sizes)):
+        for p in range(k):
+            planes.row(s, p).copy_(torch.from_numpy(peers[p][o:o + c]))
+        ws.append(torch.from_numpy(w[o:o + c].copy()).to(cuda))
+    w_full = torch.empty(n, device=cuda)
+    planes.aggregate_gather_(ws, w_full)
+    w_ref, _ = oracle.fedavg(peers, w)
+    assert np.array_equal(w_full.cpu().numpy().view(np.uint32), w_ref.view(np.uint32))
+
+
 def test_global_index_matches_device_prng_mapping():
     """Memory-sharded layout: local i -> global index == oracle.synth's chunk map."""
     plan = ChunkPlan(8 * 4 * 100, 4, 100)
@@ -213,7 +237,76 @@ def test_peer_planes_one_rank_fills_w_full():
         planes.aggregate_gather_(ws, torch.zeros(S * C - 1), reduce=lambda *a: None)
 
 
+def test_round_plane_sizes():
+    R = 256 * 8192
+    # the cfg3 tile: 8 CU rounds fill one 16-GiB plane of 256 rows exactly
+    assert sharded.round_plane_sizes(256, 125_000_000, R) == [8 * R] * 7 + [125_000_000 - 56 * R]
+    assert sharded.round_plane_sizes(256, 16 * R, R) == [8 * R] * 2          # no remainder plane
+    assert sharded.round_plane_sizes(64, 11_689_512, R) == [11_689_512]       # fits one plane
+    assert sharded.round_plane_sizes(4096, 10 * R, R) == [R] * 10              # at least one round
+    for k, n in ((256, 125_000_000), (128, 100_000_000), (16, 46_758_048)):
+        sizes = sharded.round_plane_sizes(k, n, R)
+        assert sum(sizes) == n and all(c % R == 0 for c in sizes[:-1])
+        assert all(4 * k * c <= sharded.PLANE_BYTES for c in sizes)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_peer_planes_unequal_sizes(world):
+    """Planes of unequal lengths (a short last plane): every plane's chunk
+    lands at its offset in w_full, byte-identical to the whole reduction;
+    at world 2 (gloo, in-process ranks) round s gathers G chunks of sizes[s]."""
+    k, sizes = 4, [40, 40, 13]
+    n = sum(sizes) * world
+    if world == 1:
+        results = [_unequal_planes_rank(0, 1, None, k, sizes, n)]
+    else:
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_unequal_planes_rank, args=(r, world, port, k, sizes, n, q))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        results = [q.get(timeout=120) for _ in procs]
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+    peers = [oracle.synth(n, 37, p, 1e-2) for p in range(k)]
+    w = oracle.synth(n, 37, 0xFFFFF, 5e-2)
+    want, _ = oracle.fedavg(peers, w)
+    assert all(r == want.tobytes() for r in results)
+
+
+def _unequal_planes_rank(rank, world, port, k, sizes, n, q=None):
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        peers = [oracle.synth(n, 37, p, 1e-2) for p in range(k)]
+        w = oracle.synth(n, 37, 0xFFFFF, 5e-2)
+        planes = sharded.PeerPlanes(k, 0, 0, "cpu", sizes=sizes)
+        assert planes.chunks == 3 and planes.chunk == 40 and planes.offsets == [0, 40, 80]
+        ws = []
+        for s, (o, c) in enumerate(zip(planes.offsets, planes.sizes)):
+            st = o * world + rank * c  # round s: G chunks of sizes[s], rank order
+            for p in range(k):
+                planes.row(s, p).copy_(torch.from_numpy(peers[p][st:st + c]))
+            ws.append(torch.from_numpy(w[st:st + c].copy()))
+        w_full = torch.zeros(n)
+        planes.aggregate_gather_(ws, w_full, reduce=lambda pl, s, wc, r, lr, tf: oracle_reduce(
+            [pl.row(s, p) for p in range(pl.k)], wc, r, lr, tf))
+        out = w_full.numpy().tobytes()
+        if q is not None:
+            q.put(out)
+        return out
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
 def test_peer_planes_checks_round_shapes():
+    with pytest.raises(ValueError, match="positive"):
+        sharded.PeerPlanes(3, 0, 0, "cpu", sizes=[10, 0])
     planes = sharded.PeerPlanes(3, 2, 10, "cpu")
     with pytest.raises(ValueError, match="w chunks"):
         planes.aggregate_gather_([torch.zeros(10)], reduce=lambda *a: None)

@@ -88,6 +88,52 @@ def spread(K, n, pitch, reps, dev, chunk_major_S=0):
     torch.cuda.empty_cache()
 
 
+def plane_sizes(K, n, layouts, reps, dev):
+    """The same n coordinates as chunk-major planes of different sizes (each
+    layout a list of plane lengths summing to n), carved back to back out of
+    ONE buffer so every layout reads the same memory; interleaved per rep.
+    Timing only: a layout's planes reinterpret the buffer, so outputs differ
+    between layouts (the kernels' bits are pinned by the GPU tests)."""
+    assert all(sum(L) == n for L in layouts)
+    total = max(sum(K * (c + 64) for c in L) for L in layouts) + 64
+    buf = torch.empty(total, dtype=torch.float32, device=dev)
+    step = 1 << 30
+    for i in range(0, total, step):
+        ops.fill_synthetic_(buf[i:i + step], 0x5EED0002, i // step, 1e-2)
+    w = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.fill_synthetic_(w, 0x5EED0002, 0xFFFFF, 5e-2)
+    plans = []
+    for L in layouts:
+        off, st, tabs = 0, 0, []
+        for c in L:
+            rows = [buf[off + p * (c + 64):off + p * (c + 64) + c] for p in range(K)]
+            assert all(r.numel() == c for r in rows)
+            tabs.append((st, c, ops.pointer_table(rows, dev)))
+            off += K * (c + 64)
+            st += c
+        plans.append(tabs)
+    ms = [[] for _ in layouts]
+    for _ in range(reps):
+        for i, tabs in enumerate(plans):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(1_000_000)
+            e0.record()
+            for st, c, t in tabs:
+                ops.aggregate(None, "fedavg", w=w[st:st + c], lr=0.1, table=t)
+            e1.record()
+            torch.cuda.synchronize()
+            ms[i].append(e0.elapsed_time(e1))
+    alg = 4.0 * n * (K + 2)
+    for L, v in zip(layouts, ms):
+        v = sorted(v)
+        t = v[len(v) // 2]
+        desc = " + ".join(f"{L.count(c)} x {c:,}" for c in dict.fromkeys(L))
+        print(f"K={K} n={n:,} planes {desc}: median {t:.4f} ms  {alg / t / 1e6 / 8000:.4f} of 8 TB/s  "
+              f"best {v[0]:.4f}", flush=True)
+    del buf
+    torch.cuda.empty_cache()
+
+
 def vgpr_views(reps, dev):
     """The VGPR kernel alone (fewer tiles than one split round) at K = 256 over
     row views at several offsets / pitches of one slab."""
@@ -271,6 +317,16 @@ def main():
             spread(256, 15_625_000, 15_625_064, reps, dev)   # 7 split rounds + 115 tiles + tail
             spread(256, 14_680_064, 14_680_128, reps, dev)   # exactly 7 rounds of 256 x 8192
             spread(256, 16_777_216, 16_777_280, reps, dev)   # exactly 8 rounds
+    elif mode == "wholeplanes":
+        # the cfg3 tile: 8 equal planes (each 7 split rounds + a 0.45-round
+        # VGPR remainder) against planes of whole CU rounds (256 x 8192
+        # floats) with one short last plane carrying the only remainder
+        n, R = 125_000_000, 256 * 8192
+        layouts = [[n // 8] * 8,
+                   [8 * R] * 7 + [n - 7 * 8 * R],
+                   [7 * R] * 8 + [n - 8 * 7 * R]]
+        for _ in range(3):
+            plane_sizes(256, n, layouts, reps, dev)
     elif mode == "onelaunch":
         planes_onelaunch(128, 100_000_000, 4, reps, dev)
         planes_onelaunch(256, 100_000_000, 8, reps, dev)
