@@ -246,17 +246,19 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
     # the product's memory-sharded layout (sharded.PeerPlanes): chunk-major
     # planes of K rows spanning <= 16 GB each, at least the all-gather
     # pipeline's chunks at N > 1
-    if rule == "fedavg" and world == 1 and K >= 16:
-        # one rank: planes of whole split-kernel CU rounds, one short last
-        # plane (sharded.round_plane_sizes; +1.3-1.7% on cfg3, same box)
-        sizes = sharded.round_plane_sizes(
-            K, n, torch.cuda.get_device_properties(dev).multi_processor_count * ops.SPLIT_TILE)
-    else:  # N > 1: equal chunks, the all-gather pipeline's round robin
+    # FedAvg: planes of whole split-kernel CU rounds and one short last plane
+    # (sharded.round_plane_sizes; +1.3-1.7% on cfg3, same box) when that
+    # gives the all-gather pipeline its chunks; else equal chunks
+    sizes = (sharded.round_plane_sizes(
+        K, n, torch.cuda.get_device_properties(dev).multi_processor_count * ops.SPLIT_TILE)
+        if rule == "fedavg" and K >= 16 else [])
+    if len(sizes) < (chunks if world > 1 else 1):
         S = sharded.plane_count(K, n, at_least=chunks if world > 1 else 1)
         sizes = [n // S] * S
-    # C = the longest (first) plane: the synthetic chunk map's chunk, so plane
-    # s holds global coordinates [s*C*N + rank*C, ...) -- a shorter last plane
-    # is the head of its chunk
+    # C = the longest (first) plane: the synthetic chunk map's chunk (plane s
+    # is generated as chunk s*N + rank of C; a shorter last plane as the head
+    # of its chunk -- the all-gather places it at its own offset, round s
+    # being N pieces of sizes[s])
     S, C = len(sizes), sizes[0]
     free, _ = torch.cuda.mem_get_info(dev)
     need = (K + 2 + world) * n * 4
