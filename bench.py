@@ -419,10 +419,10 @@ def plane_desc(K, sizes) -> str:
 # ------------------------------------------------------------------ cfg3 full job
 def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
     """The fixed cfg3 job: 1B coordinates x 256 peers (1.02 TB of peer data).
-    Ownership is round-robin by chunk of C = 15.625M coordinates (global
-    chunk g belongs to rank g mod N, as p2pdl_amd.sharded plans it), and each
-    rank works through its 64/N chunks in tiles of 8 chunks (125M
-    coordinates, 128 GB of peer slices -- 1.02 TB does not fit 288 GB).  Per
+    Each rank works through its 1/N of the coordinates in tiles of 125M
+    (128 GB of peer slices -- 1.02 TB does not fit 288 GB), global tile range
+    [u*T*N, (u+1)*T*N) split round-robin by plane (round s = N pieces of the
+    tile's plane s; planes of whole CU rounds, sharded.round_plane_sizes).  Per
     tile: regenerate the tile's 256 peer slices and w slice OUTSIDE the timed
     region, then reduce chunk by chunk on the compute stream while the
     all-gather of chunk s (RCCL over xGMI) runs on a second stream beside
@@ -436,8 +436,15 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
     if nchunks % (world * chunks):
         raise SystemExit(f"cfg3-full: {nchunks} chunks do not split into tiles of {chunks} over {world} GPUs")
     per = nchunks // (world * chunks)  # tiles per rank
-    planes, w = sharded.PeerPlanes(K, chunks, C, dev), pitched_slab(1, chunks, C, dev)[0]
-    wviews = [w[s, :C] for s in range(chunks)]
+    # a tile's planes: whole split-kernel CU rounds + one short last plane
+    # (sharded.round_plane_sizes, as the main line), else the 8 equal chunks
+    sizes = sharded.round_plane_sizes(
+        K, T, torch.cuda.get_device_properties(dev).multi_processor_count * ops.SPLIT_TILE)
+    if len(sizes) < chunks:
+        sizes = [C] * chunks
+    S, M = len(sizes), sizes[0]
+    planes, w = sharded.PeerPlanes(K, S, M, dev, sizes=sizes), pitched_slab(1, S, M, dev)[0]
+    wviews = [w[s, :sizes[s]] for s in range(S)]
     w_full = torch.empty(CFG3_COORDS, dtype=torch.float32, device=dev) if world > 1 else None
     tables = planes.tables
     comp = torch.cuda.current_stream(dev)
@@ -447,13 +454,15 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
     for _ in range(passes):
         w_tot = k_tot = g_tot = 0.0
         for u in range(per):
-            # local chunk s of tile u is global chunk (u*chunks + s)*N + rank: in the
-            # synthetic generator that is "rank" r + u*chunks*N of an N-rank chunk map
-            vr = rank + u * chunks * world
-            for s in range(chunks):
+            # plane s of tile u is generated as chunk (u*S + s)*N + rank of M
+            # coordinates ("rank" r + u*S*N of an N-rank chunk map; a short
+            # last plane as its head); round s's all-gather places the N
+            # pieces of sizes[s] back to back inside the tile's global range
+            vr = rank + u * S * world
+            for s in range(S):
                 for p in range(K):
-                    ops.fill_synthetic_(planes.row(s, p), seed, p, UPD_SCALE, C, world, vr + s * world)
-                ops.fill_synthetic_(w[s, :C], seed, W_PEER, W_SCALE, C, world, vr + s * world)
+                    ops.fill_synthetic_(planes.row(s, p), seed, p, UPD_SCALE, M, world, vr + s * world)
+                ops.fill_synthetic_(w[s, :sizes[s]], seed, W_PEER, W_SCALE, M, world, vr + s * world)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -466,21 +475,21 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
 
             start = torch.cuda.Event(enable_timing=True)
             start.record(comp)
-            # tile u's chunks are global rounds u*chunks .. u*chunks+chunks-1
-            tile_full = w_full[u * chunks * world * C:(u + 1) * chunks * world * C] if world > 1 else None
+            # tile u is the global range [u*T*N, (u+1)*T*N)
+            tile_full = w_full[u * T * world:(u + 1) * T * world] if world > 1 else None
             planes.aggregate_gather_(wviews, tile_full, rule="fedavg", lr=0.1, comm=comm if world > 1 else None,
                                      hook=hook)
             end = torch.cuda.Event(enable_timing=True)
             end.record(comp)
             torch.cuda.synchronize()
             w_tot += start.elapsed_time(end)
-            k_tot += sum(ev[(s, "reduce0")].elapsed_time(ev[(s, "reduce1")]) for s in range(chunks))
+            k_tot += sum(ev[(s, "reduce0")].elapsed_time(ev[(s, "reduce1")]) for s in range(S))
             if world > 1:
-                g_tot += sum(ev[(s, "gather0")].elapsed_time(ev[(s, "gather1")]) for s in range(chunks))
+                g_tot += sum(ev[(s, "gather0")].elapsed_time(ev[(s, "gather1")]) for s in range(S))
             if not checked and not args.no_check and rank == 0:
                 m = 4096
                 got = (w_full[:m] if world > 1 else w[0, :m]).cpu().numpy()  # global chunk 0: rank 0, tile 0
-                ok = bits_equal(got, oracle_expect("fedavg", K, m, seed, C, world, 0))
+                ok = bits_equal(got, oracle_expect("fedavg", K, m, seed, M, world, 0))
                 log(f"[rank 0] cfg3-full: spot check of global chunk 0 vs oracle: {'bit-exact' if ok else 'MISMATCH'}")
                 if not ok:
                     raise SystemExit("bench: cfg3-full differs from the oracle")
@@ -508,12 +517,13 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8):
         "scaling": "strong", "dtype": "fp32",
         "config": {"workload": f"cfg3 full job: fedavg over {K} peers x {CFG3_COORDS:,} fp32 coords "
                                f"({peer_bytes/1e12:.3f} TB); {per} tile(s) of {T:,} coords per GPU, "
-                               f"{chunks} chunks per tile", "tiles_per_gpu": per, "parallelism": parallelism(c)}
+                               f"{plane_desc(K, sizes)} per tile", "tiles_per_gpu": per,
+                   "parallelism": parallelism(c)}
                   | ({"per_rank": per_rank} | dist_info() if per_rank else {}) | {
                    "timing": "sum over tiles of first-kernel-start -> last-all-gather-end (HIP events; "
                              "all-gather of chunk s overlapped with chunk s+1); inputs regenerated per tile "
                              "outside the timed region (1.02 TB > 288 GB HBM)"},
-        "roofline": roofline(4 * C * (K + 2), k_ms / (per * chunks), traffic_for("cfg3-chunk", C, K)),
+        "roofline": roofline(4 * T * (K + 2) / S, k_ms / (per * S), traffic_for("cfg3-chunk", T / S, K)),
     }
 
 
