@@ -327,6 +327,13 @@ def main():
                    [7 * R] * 8 + [n - 8 * 7 * R]]
         for _ in range(3):
             plane_sizes(256, n, layouts, reps, dev)
+    elif mode == "planerounds":
+        # rounds per plane for the cfg3 tile: 4 / 8 (PLANE_BYTES, the product)
+        # / 12 / 16 whole CU rounds, one short last plane each
+        n, R = 125_000_000, 256 * 8192
+        layouts = [[r * R] * (n // (r * R)) + [n % (r * R)] for r in (8, 4, 12, 16)]
+        for _ in range(3):
+            plane_sizes(256, n, layouts, reps, dev)
     elif mode == "onelaunch":
         planes_onelaunch(128, 100_000_000, 4, reps, dev)
         planes_onelaunch(256, 100_000_000, 8, reps, dev)
