@@ -102,11 +102,19 @@ __device__ __forceinline__ void send_run(W32 dst, const T (&m)[kHalf], int lane)
 }
 
 // A raw buffer descriptor over a flat float buffer (stride 0, byte offsets;
-// dword 3 as gfx9 parts take it).  Offsets past num_records read 0 / drop
-// the store -- the callers only pass live lanes' offsets.
+// dword 3 as gfx9 parts take it).  An access past num_records reads 0 /
+// drops the store, so the range is the whole 32-bit byte space: NARROW
+// buffers (kNarrowMaxN below) keep every live lane's last byte under it --
+// the round-5 descriptor's 2^31 - 1 silently dropped coordinates >= 2^29.
+constexpr uint32_t kRsrcBytes = 0xFFFFFFFFu;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t flat_rsrc(float* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7FFFFFFF, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, kRsrcBytes, 0x00020000);
 }
+// Largest flat n the NARROW path takes: a lane's 32-bit byte offset
+// (c0 + lane) * 4 -- c0 + lane <= n - 1 + 63 -- must neither wrap nor leave
+// the descriptor's range with its 4-byte access.
+constexpr int64_t kNarrowMaxN = (int64_t(1) << 30) - 1024;
+static_assert((kNarrowMaxN - 1 + 63) * 4 + 4 <= int64_t(kRsrcBytes), "NARROW offsets inside the descriptor");
 
 __device__ __forceinline__ void block_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -392,8 +400,8 @@ __device__ __attribute__((noinline)) float pair_keys(const float* const* P, int6
   else return pair_body<RULE, kx, false, PAD>(v, im, h, lane, nullptr, P, c0, lane_off, K, pd);  // kx: max as a ^ b ^ min
 }
 
-// One 64-coordinate tile of the pair kernels.  SMALL (flat buffers below
-// 2^30 floats): the tile start rides in the 32-bit lane offset and each peer
+// One 64-coordinate tile of the pair kernels.  SMALL (flat buffers of at
+// most kNarrowMaxN floats): the tile start rides in the 32-bit lane offset and each peer
 // row's pointer is the scalar base as loaded -- no 64-bit scalar add per load
 // (256 SALU instructions per wave and tile).
 // NP wave pairs per block: pair pr takes coordinates 64 pr .. 64 pr + 63 of
@@ -423,7 +431,7 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
   // the base carries the tile start.
   // row base offset (SMALL: 0, the whole offset rides per lane; never for
   // PAD, whose pad rows are one tile wide)
-  // NARROW (SMALL flat buffers, n <= 2^30): every index a 32-bit byte
+  // NARROW (SMALL flat buffers, n <= kNarrowMaxN): every index a 32-bit byte
   // offset -- one add and one v_min_u32 per lane, and w / out are read and
   // written through buffer descriptors at that same offset (no 64-bit
   // address); the 64-bit form costs ~9 VALU more per wave.
@@ -541,7 +549,7 @@ extern "C" P2P_INTERNAL void p2p_robust_pair_launch(const float* const* peers, c
   if (tg.gx == 0) return;
   const dim3 g(tg.gx, tg.gy), b(2 * 64 * np);
   const bool pad = !(k == 2 * kHalf && (rule == P2P_RULE_MEDIAN || trim_b == 51));
-  const bool small = !segs && n <= (int64_t(1) << 30);
+  const bool small = !segs && n <= kNarrowMaxN;
 #define P2P_PAIR_ARGS g, b, 0, st, peers, segs, nseg, n, w, out, lr, ntiles, tg.gx, k, trim_b
 #define P2P_PAIR_LAUNCH(KERNEL)                                                                \
   do {                                                                                         \

@@ -132,6 +132,12 @@ class _Layout:
 
 
 _LAYOUTS = {}
+# Largest model (fp32 bytes) given a device image: each layout keeps one for
+# the life of the process, so at most two (the 'global' and 'update'
+# purposes) of this size stay on the GPU.  The cfg2 ResNet-18
+# (47 MB) and every model below it take the gather kernel; a larger model
+# (cfg3's 4 GB) takes per-tensor DMAs from its own memory.
+DEVICE_IMAGE_MAX = 1 << 30
 LOCK = threading.RLock()  # held while envelope parts (which alias the pinned buffer) are in use
 
 
@@ -157,6 +163,9 @@ def _layout_for(purpose, fast):
     if lay is None:
         devs = {t.device for _, t in fast}
         one_gpu = len(devs) == 1 and next(iter(devs)).type == "cuda"
+        # the device image stays resident with its layout (one per purpose):
+        # above DEVICE_IMAGE_MAX the tensors take one DMA each instead
+        one_gpu = one_gpu and sum(4 * t.numel() for _, t in fast) <= DEVICE_IMAGE_MAX
         lay = _Layout(sig[2], locs, any(t.is_cuda for _, t in fast), next(iter(devs)) if one_gpu else None)
         for old in [k for k in _LAYOUTS if k[0] == purpose]:
             del _LAYOUTS[old]  # one model per purpose: keep the latest layout only

@@ -38,6 +38,7 @@ from __future__ import annotations
 import ctypes
 import os
 import pickle
+import re
 import struct
 import threading
 from collections import OrderedDict, deque
@@ -99,11 +100,32 @@ class RawTensor:
         """A torch tensor holding a copy of the payload, of the storage's
         dtype (bfloat16 from its bit patterns), on ``device`` (default: the
         storage's own location, as ``pickle.loads`` restores it)."""
+        dev = device_of_location(self.storage.location) if device is None else device
         t = torch.from_numpy(np.array(self.array()))
         if self.storage.dtype is np.uint16:
             t = t.view(torch.bfloat16)
-        dev = self.storage.location if device is None else device
         return t if str(dev) == "cpu" else t.to(dev)
+
+
+_LOCATION = re.compile(r"cpu|cuda(?::(\d{1,4}))?")
+
+
+def device_of_location(location: str) -> str:
+    """A peer's storage location as a device this process has: 'cpu', or
+    'cuda' / 'cuda:<i>' with i below the visible device count (torch's own
+    restore raises RuntimeError for a missing device).  Anything else raises
+    pickle.UnpicklingError, the documented error for a peer's malformed
+    bytes.  Checked where a tensor is materialised: the parsers
+    (this module's and wire.cpp's, which must agree) keep the string, and a
+    landed update's tensors go to the inbox's device whatever it names."""
+    m = _LOCATION.fullmatch(location) if isinstance(location, str) else None
+    if m is None:
+        raise pickle.UnpicklingError(f"unsupported storage location {location!r}")
+    if location != "cpu":
+        i = int(m.group(1) or 0)
+        if i >= torch.cuda.device_count():
+            raise pickle.UnpicklingError(f"storage location {location!r}: no such device here")
+    return location
 
 
 class _Mark:
@@ -649,6 +671,9 @@ def _detached(v):
         d = OrderedDict() if isinstance(v, OrderedDict) else {}
         for a, b in dict.items(v):
             d[_detached(a)] = _detached(b)
+        meta = getattr(v, "__dict__", {}).get("_metadata") if isinstance(v, OrderedDict) else None
+        if meta is not None:  # BUILD's only attribute: load_state_dict reads it (node.py:244)
+            d._metadata = _detached(meta)
         return d
     return v
 

@@ -108,6 +108,25 @@ class PeerPlanes:
     def row(self, s: int, p: int) -> torch.Tensor:
         return self.data[s, p, :self.sizes[s]]
 
+    def global_range(self, s: int, rank: int, world: int) -> tuple[int, int]:
+        """(global start, length) of rank's plane s in the gathered model:
+        round s gathers every rank's chunk s, in rank order, to
+        w_full[offsets[s]*G, (offsets[s]+sizes[s])*G), so rank r's lands at
+        offsets[s]*G + r*sizes[s].  With equal planes that is ChunkPlan's
+        round robin (global chunk s*G + r); with unequal ones (a short last
+        plane, ``round_plane_sizes``) it is NOT -- producers scatter their
+        updates into ``row(s, p)`` by this mapping."""
+        if not (0 <= s < self.chunks and 0 <= rank < world):
+            raise IndexError(f"plane {s} of {self.chunks}, rank {rank} of {world}")
+        return self.offsets[s] * world + rank * self.sizes[s], self.sizes[s]
+
+    def global_index(self, s: int, rank: int, world: int, i: int) -> int:
+        """Global coordinate of element i of rank's plane s (``global_range``)."""
+        st, ln = self.global_range(s, rank, world)
+        if not 0 <= i < ln:
+            raise IndexError(i)
+        return st + i
+
     def reduce_(self, s: int, w: torch.Tensor, rule="fedavg", *, lr: float = 0.1,
                 trim_frac: float = 0.2) -> None:
         from . import ops
@@ -118,8 +137,9 @@ class PeerPlanes:
                           rule="fedavg", lr: float = 0.1, trim_frac: float = 0.2, group=None,
                           comm=None, reduce: Callable | None = None, hook: Callable | None = None) -> None:
         """One aggregation round over every plane.  ``ws[s]`` is this rank's
-        chunk s of w -- global chunk s*G + rank (ChunkPlan's round robin) --
-        updated in place.  With ``w_full`` and an initialised process group,
+        chunk s of w -- global coordinates ``global_range(s, rank, G)``, which
+        for equal planes is global chunk s*G + rank (ChunkPlan's round robin)
+        -- updated in place.  With ``w_full`` and an initialised process group,
         round s's all-gather writes every rank's chunk s to the contiguous
         w_full[o*G, (o+C)*G) (o, C = offsets[s], sizes[s]; equal planes:
         [s*G*C, (s+1)*G*C)): on ``comm`` (a second stream) beside plane

@@ -188,3 +188,20 @@ def test_envelope_large_gpu_tensors_settle_before_the_parts_are_read(cuda):
         upd = pickle.loads(E.dumps_state(sd))
         for k, v in sd.items():
             assert torch.equal(got[k], v) and torch.equal(upd[k], v), (rnd, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("image_max", [0, 1 << 30])
+def test_envelope_device_image_only_below_the_cap(cuda, monkeypatch, image_max):
+    """a layout's device image stays resident, so models above
+    DEVICE_IMAGE_MAX take per-tensor DMAs (no image); both routes give the
+    reference's bytes."""
+    monkeypatch.setattr(E, "DEVICE_IMAGE_MAX", image_max)
+    monkeypatch.setattr(E, "_LAYOUTS", {})
+    net = torch.nn.Sequential(torch.nn.Linear(33, 64), torch.nn.BatchNorm1d(64), torch.nn.Linear(64, 10)).to(cuda)
+    sd = net.state_dict()
+    got = pickle.loads(E.global_model_envelope(sd, "a", 2))["model"]
+    (lay,) = E._LAYOUTS.values()
+    assert (lay.dev is None) == (image_max == 0)
+    for k, v in sd.items():
+        assert got[k].device == v.device and torch.equal(got[k], v), k

@@ -1013,6 +1013,41 @@ def test_robust_many_peers_beyond_2g_aliased_views(cuda, k, rule, n):
     assert_bits_equal(got, want, what=f"{rule} K={k} n={n} aliased")
 
 
+@pytest.mark.parametrize("rule", ["median", "trimmed"])
+@pytest.mark.parametrize("n", [(1 << 29) + 4099, (1 << 30) - 1024, (1 << 30) - 1023])
+def test_robust_narrow_path_past_2g_bytes(cuda, rule, n):
+    """the K = 256 flat pair kernels' NARROW path reads
+    and writes w / out through a raw buffer descriptor at 32-bit byte
+    offsets; with a 2**31 - 1 B range every coordinate >= 2**29 was silently
+    left unwritten.  n up to the NARROW bound (2**30 - 1024, robust_pair.hip
+    kNarrowMaxN) and one past it (the 64-bit path), w AND out written,
+    sampled around 2**29 and both ends against the oracle.  Peers alias one
+    buffer shifted by 64 floats, as in the test above."""
+    k, shift, seed = 256, 64, 0x5EED00B4
+    buf = torch.empty(n + (k - 1) * shift, dtype=torch.float32, device=cuda)
+    ops.fill_synthetic_(buf, seed, 0, 1e-2)
+    peers = [buf[p * shift:p * shift + n] for p in range(k)]
+    w = torch.empty(n, dtype=torch.float32, device=cuda)
+    ops.fill_synthetic_(w, seed, 0xFFFFF, 5e-2)
+    out = torch.empty(n, dtype=torch.float32, device=cuda)
+    out.fill_(float("nan"))
+    ops.aggregate(peers, rule, w=w, out=out, lr=0.1)
+    rng = np.random.default_rng(13)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 2000), np.arange(256), n - 1 - np.arange(1100),
+                                    (1 << 29) - 70 + np.arange(140)]))
+    idx = idx[idx < n]
+    sel = torch.from_numpy(idx).to(cuda)
+    got_w, got_o = w[sel].cpu().numpy(), out[sel].cpu().numpy()
+    del peers, buf, out, w
+    torch.cuda.empty_cache()
+    x = [oracle.synth_at(idx + p * shift, seed, 0, 1e-2) for p in range(k)]
+    w0 = oracle.synth_at(idx, seed, 0xFFFFF, 5e-2)
+    r = ops.rule_id(rule)
+    want_w, want_o = oracle.robust(x, r, ops.trim_count(k) if r == 2 else 0, w=w0)
+    assert_bits_equal(got_o, want_o, what=f"{rule} out n={n}")
+    assert_bits_equal(got_w, want_w, what=f"{rule} w n={n}")
+
+
 def test_delta_beyond_2g_elements_sampled(cuda):
     n, seed = BIG_N, 0x5EED00B2
     cur = torch.empty(n, dtype=torch.float32, device=cuda)

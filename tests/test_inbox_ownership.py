@@ -172,6 +172,51 @@ def test_global_model_update_16bit_tensors_decode(pageable):
         assert got[k].dtype == sd[k].dtype and torch.equal(got[k], sd[k]), k
 
 
+def test_global_model_update_keeps_state_dict_metadata(pageable):
+    """a real state_dict's _metadata (module versions, which
+    load_state_dict reads at node.py:244, e.g. BatchNorm's) survives
+    open_envelope as it survives pickle.loads."""
+    m = torch.nn.Sequential(torch.nn.Linear(3, 2), torch.nn.BatchNorm1d(2))
+    sd = m.state_dict()
+    data = pickle.dumps({"type": "global_model_update", "model": sd, "addr": "a", "port": 1})
+    got = open_envelope(message(pageable, data))["model"]
+    want = pickle.loads(data)["model"]
+    assert got._metadata == want._metadata == sd._metadata
+    m.load_state_dict(got)  # the reference's use of it
+
+
+def _tensor_at(location: str, n: int = 4):
+    """A pickled fp32 tensor whose legacy storage blob names `location` (the
+    record a peer writes; envelope.legacy_storage_header)."""
+    from p2pdl_amd.node import envelope as E
+
+    blob = E.legacy_storage_header(n, "0", location) + np.arange(n, dtype=np.float32).tobytes()
+
+    class Storage:
+        def __reduce__(self):
+            return (torch.storage._load_from_bytes, (blob,))
+
+    class Tensor:
+        def __reduce__(self):
+            return (torch._utils._rebuild_tensor_v2, (Storage(), 0, (n,), (1,), False, collections.OrderedDict()))
+
+    return Tensor()
+
+
+@pytest.mark.parametrize("location", ["cuda:99", "garbage", "cuda:0:1", "cuda:-1", "meta"])
+def test_bad_storage_location_is_an_unpickling_error(pageable, location):
+    """a peer naming a missing or malformed device raises the
+    documented pickle.UnpicklingError, not RuntimeError from the tensor's
+    materialisation."""
+    data = pickle.dumps({"type": "global_model_update", "addr": "a", "port": 1,
+                         "model": collections.OrderedDict(w=_tensor_at(location))})
+    with pytest.raises(pickle.UnpicklingError):
+        open_envelope(message(pageable, data))
+    ok = pickle.dumps({"type": "global_model_update", "addr": "a", "port": 1,
+                       "model": collections.OrderedDict(w=_tensor_at("cpu"))})
+    assert torch.equal(open_envelope(message(pageable, ok))["model"]["w"], torch.arange(4.0))
+
+
 def test_pool_is_bounded_by_bytes():
     pool = DeviceInbox.__new__(DeviceInbox)  # the pool's state only
     pool._lock, pool._pinned_free, pool.pool_bytes = threading.Lock(), [], 1000

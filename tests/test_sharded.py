@@ -288,7 +288,9 @@ def _unequal_planes_rank(rank, world, port, k, sizes, n, q=None):
         assert planes.chunks == 3 and planes.chunk == 40 and planes.offsets == [0, 40, 80]
         ws = []
         for s, (o, c) in enumerate(zip(planes.offsets, planes.sizes)):
-            st = o * world + rank * c  # round s: G chunks of sizes[s], rank order
+            st, ln = planes.global_range(s, rank, world)
+            assert (st, ln) == (o * world + rank * c, c)  # round s: G chunks of sizes[s], rank order
+            assert planes.global_index(s, rank, world, c - 1) == st + c - 1
             for p in range(k):
                 planes.row(s, p).copy_(torch.from_numpy(peers[p][st:st + c]))
             ws.append(torch.from_numpy(w[st:st + c].copy()))
@@ -302,6 +304,18 @@ def _unequal_planes_rank(rank, world, port, k, sizes, n, q=None):
     finally:
         if world > 1:
             dist.destroy_process_group()
+
+
+def test_peer_planes_global_range_equal_planes_is_the_round_robin():
+    """Equal planes: global_range(s, r, G) is ChunkPlan's global chunk s*G + r."""
+    planes = sharded.PeerPlanes(2, 3, 10, "cpu")
+    plan = sharded.ChunkPlan(3 * 10 * 4, 4, 10)
+    for r in range(4):
+        assert [planes.global_range(s, r, 4) for s in range(3)] == plan.owned(r)
+    with pytest.raises(IndexError):
+        planes.global_range(3, 0, 4)
+    with pytest.raises(IndexError):
+        planes.global_index(0, 0, 4, 10)
 
 
 def test_peer_planes_checks_round_shapes():
