@@ -42,8 +42,10 @@ extern "C" {
  * 6: adds p2p_fedavg_split_plan / p2p_fedavg_split_segments_f32 (whole
  *    tiles of a state_dict on the LDS-DMA split kernel).
  * 7: adds p2p_fedavg_split_rows_f32 / p2p_row_chunk_t (a state_dict slab's
- *    rows as flat peers, the model scattered by 1024-float chunks). */
-#define P2P_ABI_VERSION 7
+ *    rows as flat peers, the model scattered by 1024-float chunks).
+ * 8: adds p2p_fedavg_split_chunks_f32 (a state_dict of separately allocated
+ *    tensors on the split kernel, one launch, by 1024-float chunks). */
+#define P2P_ABI_VERSION 8
 
 typedef void *p2p_stream_t; /* hipStream_t */
 
@@ -156,6 +158,21 @@ typedef struct {
 } p2p_row_chunk_t;
 int32_t p2p_fedavg_split_rows_f32(const float *const *rows, int32_t k, int64_t ntiles, const p2p_row_chunk_t *chunks,
                                   int32_t rule, float lr, p2p_stream_t stream);
+
+/* FedAvg over a whole state_dict of separately allocated tensors -- what the
+ * reference's receive path hands aggregate_models (node/node.py:138-141
+ * pickle.loads, aggregator/aggregation.py:25-38) -- on the split kernel in
+ * ONE launch.  `chunks` (DEVICE, ntiles * 8 entries) lists P2P_ROW_CHUNK-
+ * element chunks of the segments of `segs`: entry c names segment `seg` (-1:
+ * padding, no work) and the chunk's first element `c0` (a multiple of 4) in
+ * it; the chunk covers elements [c0, c0 + min(P2P_ROW_CHUNK, n - c0)).
+ * Split tile t is chunks 8t .. 8t + 7.  Every listed segment's K peer
+ * pointers and w / out must be 16-byte aligned (the caller's check); a
+ * segment's tile_begin is not read.  No read leaves a segment's tensors.
+ * Same per-element op order as p2p_fedavg_apply_f32 (FedAvg rules only).
+ * ABI 8. */
+int32_t p2p_fedavg_split_chunks_f32(const p2p_split_tile_t *chunks, int64_t ntiles, const p2p_segment_t *segs,
+                                    int32_t k, int32_t rule, float lr, p2p_stream_t stream);
 
 /* Whole state_dict in ONE launch: segs is a DEVICE array of nseg entries
  * (tile_begin prefix-summed with p2p_tile_elems(rule, k)); total_tiles is the

@@ -164,3 +164,48 @@ def sha256(messages, target_s: float) -> dict:
     reps1, el1 = run(1, max(1.0, target_s / 3))
     return dict(info, value=nbytes * reps / el / 1e9, value_1thread=nbytes * reps1 / el1 / 1e9, reps=reps,
                 seconds=round(el, 2), reps_1thread=reps1)
+
+
+def arrival(messages, expected, w: "torch.Tensor", target_s: float) -> dict:
+    """cfg5 as the reference's node receives it, on the host: SHA-256 of every
+    serialized update (hashlib, utils/crypto.py:56 -- with a thread pool of
+    the host thread count, then one thread), the updates whose digest matches
+    what the sender signed unpickled (node/node.py:138 pickle.loads: CPU
+    tensors) and the reference's FedAvg op sequence over them
+    (aggregator/aggregation.py:15-38, torch intra-op threads = the host
+    thread count, then one).  value = hashed bytes per second (GB/s)."""
+    import pickle
+
+    info = host_threads()
+    nbytes = float(sum(map(len, messages)))
+    w0 = w.clone()
+
+    def one(ex):
+        ds = list(ex.map(lambda m: hashlib.sha256(m).digest(), messages)) if ex else \
+            [hashlib.sha256(m).digest() for m in messages]
+        acc = [pickle.loads(m)["w"] for m, d, e in zip(messages, ds, expected) if d == e]
+        w.copy_(w0)
+        reference_ops_fedavg_(w, acc)
+        return len(acc)
+
+    def run(threads, secs):
+        prev = torch.get_num_threads()
+        torch.set_num_threads(threads)
+        try:
+            with ThreadPoolExecutor(threads) as ex:
+                pool = ex if threads > 1 else None
+                one(pool)
+                reps, t0 = 0, time.perf_counter()
+                while True:
+                    n_acc = one(pool)
+                    reps += 1
+                    el = time.perf_counter() - t0
+                    if el >= secs:
+                        return reps, el, n_acc
+        finally:
+            torch.set_num_threads(prev)
+
+    reps, el, n_acc = run(info["threads"], target_s)
+    reps1, el1, _ = run(1, max(1.0, target_s / 3))
+    return dict(info, value=nbytes * reps / el / 1e9, value_1thread=nbytes * reps1 / el1 / 1e9, reps=reps,
+                seconds=round(el, 2), reps_1thread=reps1, accepted=n_acc)

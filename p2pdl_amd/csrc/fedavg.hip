@@ -25,6 +25,8 @@
 // 6.2-6.4 TB/s = 78-80% of 8 TB/s.  No inter-block reuse exists, so no XCD
 // remap is needed (guide T1: 0% on elementwise).
 #include <atomic>
+#include <map>
+#include <mutex>
 
 #include "p2p_common.h"
 
@@ -301,13 +303,32 @@ __device__ __forceinline__ SplitTile split_tile(const float* const* peers, float
   }
 }
 
+// The consumer side of one tile: K stages added in peer order from +0 (:15,
+// :25-28), one barrier per stage; `hook(k)` runs right after barrier k (the
+// tile queue's publication, QUEUE below; a no-op otherwise).
+template <typename Hook>
+__device__ __forceinline__ void sum_stages(f4 (&acc)[kSRpw], int K, uint32_t lds0, uint32_t mine, int& slot,
+                                           Hook&& hook) {
+#pragma unroll
+  for (int r = 0; r < kSRpw; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
+  for (int k = 0; k < K; ++k) {
+    __builtin_amdgcn_s_barrier();
+    hook(k);
+    f4 x[kSRpw];
+    lds_read4(x, lds0 + static_cast<uint32_t>(slot) * (kSTile * 4) + mine);
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r) acc[r] += x[r];  // strictly in list order (:25-28)
+    slot = slot + 1 == kSS ? 0 : slot + 1;
+  }
+}
+
 // One ROWS tile of consumer wave cw: its chunk's w slice DMA'd beside the
 // stages (lanes inside the chunk's valid floats only), the K stages added in
 // peer order, then / K and the apply where the chunk holds model floats --
 // element-wise for the float4 that straddles the key's end.
-template <bool RECIP>
+template <bool RECIP, typename Hook>
 __device__ __forceinline__ void rows_tile(const p2p_row_chunk_t* ch, int K, int lane, float lr, float fk, float inv,
-                                          float* lds, uint32_t lds0, uint32_t mine, int& slot, int cw) {
+                                          float* lds, uint32_t lds0, uint32_t mine, int& slot, int cw, Hook&& hook) {
   float* cwp = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&ch->w))));
   const int64_t valid = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&ch->valid))));
   if (cwp) {
@@ -318,16 +339,7 @@ __device__ __forceinline__ void rows_tile(const p2p_row_chunk_t* ch, int K, int 
     }
   }
   f4 acc[kSRpw];
-#pragma unroll
-  for (int r = 0; r < kSRpw; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
-  for (int k = 0; k < K; ++k) {
-    __builtin_amdgcn_s_barrier();
-    f4 x[kSRpw];
-    lds_read4(x, lds0 + static_cast<uint32_t>(slot) * (kSTile * 4) + mine);
-#pragma unroll
-    for (int r = 0; r < kSRpw; ++r) acc[r] += x[r];  // strictly in list order (:25-28)
-    slot = slot + 1 == kSS ? 0 : slot + 1;
-  }
+  sum_stages(acc, K, lds0, mine, slot, hook);
   if (!cwp) return;  // padding between keys: averaged, dropped
   f4 m[kSRpw];
 #pragma unroll
@@ -347,55 +359,227 @@ __device__ __forceinline__ void rows_tile(const p2p_row_chunk_t* ch, int K, int 
   }
 }
 
-// SEGS: the host lists only whole tiles of segments whose K peer pointers and
-// w / out are all 16-B aligned (ops.py checks them when it builds the list);
-// a flat buffer is checked here.
+// CHUNKS (round 6): a state_dict of separately allocated tensors -- the
+// reference caller's pickle.loads dicts (node/node.py:138-141) -- in ONE
+// launch.  Split tile t is the 8 chunks list[8t .. 8t + 7]; chunk c names
+// segment seg (-1: padding) and its first element c0, and holds the
+// segment's floats [c0, c0 + valid), valid = min(1024, n - c0).  Loader wave
+// wv streams chunks 2wv and 2wv + 1 of each stage, each from its own key's
+// peer pointer, through a buffer descriptor whose range ends at the chunk's
+// last whole float4: the lanes past it issue no memory request (an
+// out-of-range buffer access), every wave still issues exactly kSPer DMAs
+// per stage (the vmcnt arithmetic holds), and no read leaves a tensor.
+// Consumer wave c owns chunk c of the tile, as in ROWS; the one float4 that
+// straddles a key's end (n % 4 != 0) is summed element by element from the
+// peers in list order (the same op order as fedavg_elem).
+struct ChunkSrc {
+  const float* const* peers;  // the key's K peer pointers (nullptr: padding)
+  int64_t c0;                 // the chunk's first element in the key
+  uint32_t bytes;             // the DMA range: the chunk's whole float4s, in bytes
+};
+__device__ __forceinline__ ChunkSrc chunk_src(const p2p_split_tile_t* list, const Seg* segs, int64_t c) {
+  const int64_t seg = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&list[c].seg))));
+  if (seg < 0) return ChunkSrc{nullptr, 0, 0u};
+  const int64_t c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&list[c].c0))));
+  const Seg* sp = segs + seg;
+  const int64_t n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
+  const int64_t valid = n - c0 < P2P_ROW_CHUNK ? n - c0 : P2P_ROW_CHUNK;
+  return ChunkSrc{reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->peers)))), c0,
+                  static_cast<uint32_t>((valid & ~int64_t(3)) * 4)};
+}
+constexpr int kChunkDma = P2P_ROW_CHUNK / 256;  // 1-KiB DMAs per chunk per stage
+static_assert(kSPer == 2 * kChunkDma, "a loader wave streams two chunks per stage");
+// Peer ki's part of chunk cs into LDS float offset `dst`: kChunkDma buffer
+// DMAs (nt), lanes past the range masked by the descriptor.  A padding chunk
+// gets an empty range over a valid base (the list itself): no request at all.
+__device__ __forceinline__ void chunk_dma(const ChunkSrc& cs, int ki, const void* any, float* dst, int lane) {
+  const float* src = cs.bytes ? table_at(cs.peers, ki) + cs.c0 : static_cast<const float*>(any);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), 0, cs.bytes, 0x00020000);
+#pragma unroll
+  for (int q = 0; q < kChunkDma; ++q)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (P2P_LDS void*)(dst + q * 256), 16, (q * 256 + lane * 4) * 4, 0, 0,
+                                             2 /* nt */);
+}
+
+// One CHUNKS tile of consumer wave cw (see above).
+template <bool RECIP, typename Hook>
+__device__ __forceinline__ void chunks_tile(const p2p_split_tile_t* list, const Seg* segs, int64_t c, int K, int lane,
+                                            float lr, float fk, float inv, float* lds, uint32_t lds0, uint32_t mine,
+                                            int& slot, int cw, Hook&& hook) {
+  const int64_t seg = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&list[c].seg))));
+  const float* const* cp = nullptr;
+  float *cwp = nullptr, *cop = nullptr;
+  int64_t c0 = 0, valid = 0;
+  if (seg >= 0) {
+    const Seg* sp = segs + seg;
+    c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&list[c].c0))));
+    const int64_t n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
+    valid = n - c0 < P2P_ROW_CHUNK ? n - c0 : P2P_ROW_CHUNK;
+    cp = reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->peers))));
+    float* wb = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->w))));
+    float* ob = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->out))));
+    cwp = wb ? wb + c0 : nullptr;
+    cop = ob ? ob + c0 : nullptr;
+  }
+  if (cwp) {
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r) {
+      const int idx = lane * 4 + r * 256;
+      if (idx + 4 <= valid) dma16<0>(cwp + idx, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
+    }
+  }
+  f4 acc[kSRpw];
+  sum_stages(acc, K, lds0, mine, slot, hook);
+  if (valid <= 0) return;  // padding
+  f4 m[kSRpw];
+#pragma unroll
+  for (int r = 0; r < kSRpw; ++r) m[r] = div4<RECIP>(acc[r], fk, inv);  // (:31-32)
+  if (cop) {
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r)
+      if (lane * 4 + r * 256 + 4 <= valid) st(cop + lane * 4 + r * 256, m[r]);
+  }
+  if (cwp) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w DMA (and its older stores)
+    f4 wq[kSRpw];
+    lds_read4(wq, lds0 + static_cast<uint32_t>(kSS * kSTile * 4) + mine);
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r)
+      if (lane * 4 + r * 256 + 4 <= valid) st(cwp + lane * 4 + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
+  }
+  if (valid & 3) {  // the key's last, partial float4: its lane sums it from the peers themselves
+    const int idx = static_cast<int>(valid & ~int64_t(3));
+    if (lane == (idx & 255) >> 2) {
+      float* wq = cwp ? cwp - c0 : nullptr;
+      float* oq = cop ? cop - c0 : nullptr;
+      for (int64_t i = c0 + idx; i < c0 + valid; ++i) fedavg_elem<RECIP>(cp, K, i, wq, oq, lr);
+    }
+  }
+}
+
+// One FLAT / SEGS tile of consumer wave cw: the w slice DMA'd beside the
+// stages, the K stages, / K, the mean stored (out) and the apply (w).
+template <bool RECIP, typename Hook>
+__device__ __forceinline__ void flat_tile(const SplitTile& tl, int K, int lane, float lr, float fk, float inv,
+                                          float* lds, uint32_t lds0, uint32_t mine, int& slot, int cw, Hook&& hook) {
+  const int64_t o = tl.c0 + cw * kSRpw * 256 + lane * 4;
+  if (tl.w) {
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r) dma16<0>(tl.w + o + r * 256, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
+  }
+  f4 acc[kSRpw];
+  sum_stages(acc, K, lds0, mine, slot, hook);
+  f4 m[kSRpw];
+#pragma unroll
+  for (int r = 0; r < kSRpw; ++r) m[r] = div4<RECIP>(acc[r], fk, inv);  // (:31-32)
+  if (tl.out) {
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r) st(tl.out + o + r * 256, m[r]);
+  }
+  if (tl.w) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w DMA (and its older stores)
+    f4 wq[kSRpw];
+    lds_read4(wq, lds0 + static_cast<uint32_t>(kSS * kSTile * 4) + mine);
+#pragma unroll
+    for (int r = 0; r < kSRpw; ++r) st(tl.w + o + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
+  }
+}
+
+// The kernel's modes.  FLAT: a flat buffer, tile t at t * kSTile (the host
+// takes whole tiles).  SEGS: the host lists only whole tiles of segments
+// whose K peer pointers and w / out are all 16-B aligned (ops.py checks them
+// when it builds the list); a flat buffer is checked here.
 // ROWS (round 5): the peers are the K rows of a state_dict slab (DeviceInbox)
 // read as flat buffers -- every tile a whole one -- and the model is
 // scattered: consumer wave c of tile t applies to chunks[8t + c], the w
 // tensor (if any) holding the row's floats [1024(8t + c), +1024) and how
 // many of them it holds (keys start on 1024-float boundaries; the padding
 // between them is averaged and dropped).  The host checks the alignment.
-template <bool RECIP, bool SEGS, bool ROWS = false>
+// CHUNKS: `tiles` is the chunk list (8 entries per tile), see above; the
+// host checks the alignment of every listed key.
+enum SplitMode { kFlat = 0, kSegs = 1, kRows = 2, kChunks = 3 };
+
+// QUEUE (round 6, tools/split_fixed_lab.hip variant Q): a persistent grid
+// of min(tiles, CUs) blocks that claim their tiles from a per-stream counter
+// (`queue`: [claims, blocks done], zero at launch start) instead of one
+// block per tile.  A block's loaders then stream tile j+1's first stages
+// during tile j's epilogue (w DMA wait, / K, apply, stores), which a
+// one-tile block leaves the CU idle for.  Consumer wave 0 claims the next
+// tile (a vector atomic) when it starts a tile and publishes it in LDS after
+// the tile's barrier kQW; every wave reads it after barrier kQR (loaders) or
+// after the tile (consumers), so the loaders know the next tile -- or that
+// there is none: the same barrier count on both sides -- before its first
+// stage is due ((j+1)K - kSS + 1 > jK + kQR for K >= 8).  The last block to
+// finish zeroes the counter for the stream's next launch.
+constexpr int kQW = 2, kQR = 4;
+constexpr int kQueueMinK = kQR + kSS;  // K the queue's publication schedule needs
+
+template <bool RECIP, int MODE, bool QUEUE = false>
 __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const float* const* __restrict__ peers,
                                                                         int K, const int32_t* k_dev,
                                                                         int64_t ntiles, float* w, float* out,
                                                                         float lr, const p2p_split_tile_t* tiles,
                                                                         const Seg* segs,
-                                                                        const p2p_row_chunk_t* chunks = nullptr) {
-  static_assert(!(SEGS && ROWS), "one mode");
+                                                                        const p2p_row_chunk_t* chunks = nullptr,
+                                                                        int32_t* queue = nullptr) {
+  constexpr bool SEGS = MODE == kSegs;
   __shared__ __attribute__((aligned(16))) float lds[(kSS + 1) * kSTile];
+  __shared__ int64_t tq[4];
   if (k_dev) K = __builtin_amdgcn_readfirstlane(ldg(k_dev));
   if (K <= 0) return;
   const int64_t G = gridDim.x, b = bid_x();
   const int wv = __builtin_amdgcn_readfirstlane(tid_x() >> 6), lane = tid_x() & 63;
-  if (!SEGS && !ROWS && !all_aligned16(peers, K, w, out)) {
+  if (MODE == kFlat && !all_aligned16(peers, K, w, out)) {
     // 4-B-aligned views: element-wise, same op order, no LDS (block-uniform)
     constexpr int kT = 64 * (kSL + kSC);
     for (int64_t t = b; t < ntiles; t += G)  // 11 x 768 >= 8192: the tile's end bounds the last
       fedavg_scalar<(kSTile + kT - 1) / kT, RECIP>(peers, K, (t + 1) * kSTile, t * kSTile + tid_x(), kT, w, out, lr);
     return;
   }
-  const int64_t N = (ntiles - b + G - 1) / G * K;  // stages (= barriers) of this block
   if (wv < kSL) {
-    int64_t ti = b, issued = 0;
-    int ki = 0, si = 0;
-    SplitTile tl = split_tile<SEGS>(peers, w, out, tiles, segs, ti);
+    // stages (= barriers) of this block: known up front for a static tile
+    // set (b, b + G, ...); grown tile by tile from the queue otherwise
+    int64_t N = QUEUE ? K : (ntiles - b + G - 1) / G * K;
+    int64_t ti = b, tnext = ntiles, issued = 0;
+    int ki = 0, si = 0, kb = 0, jb = 0;  // barrier k of the block's tile jb
+    SplitTile tl{};
+    ChunkSrc c0{}, c1{};
     auto issue = [&]() {
-      if (ki == 0 && issued > 0) tl = split_tile<SEGS>(peers, w, out, tiles, segs, ti);
-      const float* src = table_at(tl.peers, ki) + tl.c0 + (wv * kSPer) * 256 + lane * 4;
+      if (ki == 0) {  // a new tile
+        if (issued > 0) ti = QUEUE ? tnext : ti + G;
+        if constexpr (MODE == kChunks) {
+          c0 = chunk_src(tiles, segs, ti * kSC + 2 * wv);
+          c1 = chunk_src(tiles, segs, ti * kSC + 2 * wv + 1);
+        } else {
+          tl = split_tile<SEGS>(peers, w, out, tiles, segs, ti);
+        }
+      }
+      float* dst = &lds[si * kSTile + wv * kSPer * 256];
+      if constexpr (MODE == kChunks) {
+        chunk_dma(c0, ki, tiles, dst, lane);
+        chunk_dma(c1, ki, tiles, dst + kChunkDma * 256, lane);
+      } else {
+        const float* src = table_at(tl.peers, ki) + tl.c0 + (wv * kSPer) * 256 + lane * 4;
 #pragma unroll
-      for (int q = 0; q < kSPer; ++q) dma16<2 /* nt */>(src + q * 256, &lds[si * kSTile + (wv * kSPer + q) * 256]);
+        for (int q = 0; q < kSPer; ++q) dma16<2 /* nt */>(src + q * 256, dst + q * 256);
+      }
       ++issued;
       si = si + 1 == kSS ? 0 : si + 1;
-      if (++ki == K) { ki = 0; ti += G; }
+      if (++ki == K) ki = 0;
     };
     for (int d = 0; d < kSS - 1 && issued < N; ++d) issue();
     for (int64_t i = 0; i < N; ++i) {
       if (i + kSS - 2 < N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kSS - 2) * kSPer) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // stage i landed; stage i-1's slot read
-      if (issued < N) issue();       // into that slot
+      if constexpr (QUEUE) {
+        if (kb == kQR) {  // the block's next tile, published after barrier kQW of this one
+          tnext = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(tq[(jb + 1) & 3])));
+          if (tnext < ntiles) N += K;
+        }
+        if (++kb == K) { kb = 0; ++jb; }
+      }
+      if (issued < N) issue();  // into that slot
     }
     return;
   }
@@ -405,41 +589,35 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
   const float fk = static_cast<float>(K);
   const float inv = RECIP ? 1.0f / fk : 0.f;
   int slot = 0;
-  for (int64_t t = b; t < ntiles; t += G) {
-    if constexpr (ROWS) {
-      rows_tile<RECIP>(chunks + t * kSC + cw, K, lane, lr, fk, inv, lds, lds0, mine, slot, cw);
-      continue;
+  auto tile = [&](int64_t t, auto&& hook) {
+    if constexpr (MODE == kRows)
+      rows_tile<RECIP>(chunks + t * kSC + cw, K, lane, lr, fk, inv, lds, lds0, mine, slot, cw, hook);
+    else if constexpr (MODE == kChunks)
+      chunks_tile<RECIP>(tiles, segs, t * kSC + cw, K, lane, lr, fk, inv, lds, lds0, mine, slot, cw, hook);
+    else
+      flat_tile<RECIP>(split_tile<SEGS>(peers, w, out, tiles, segs, t), K, lane, lr, fk, inv, lds, lds0, mine, slot,
+                       cw, hook);
+  };
+  if constexpr (!QUEUE) {
+    for (int64_t t = b; t < ntiles; t += G) tile(t, [](int) {});
+    return;
+  } else {
+    int64_t t = b;
+    for (int j = 0;; ++j) {
+      int64_t claim = 0;
+      if (cw == 0 && lane == 0) claim = G + atomicAdd(&queue[0], 1);
+      tile(t, [&](int k) {
+        if (k == kQW && cw == 0) {
+          if (lane == 0) tq[(j + 1) & 3] = claim;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+      });
+      t = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(tq[(j + 1) & 3])));
+      if (t >= ntiles) break;
     }
-    const SplitTile tl = split_tile<SEGS>(peers, w, out, tiles, segs, t);
-    const int64_t o = tl.c0 + cw * kSRpw * 256 + lane * 4;
-    if (tl.w) {
-#pragma unroll
-      for (int r = 0; r < kSRpw; ++r) dma16<0>(tl.w + o + r * 256, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
-    }
-    f4 acc[kSRpw];
-#pragma unroll
-    for (int r = 0; r < kSRpw; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};  // +0 init (:15)
-    for (int k = 0; k < K; ++k) {
-      __builtin_amdgcn_s_barrier();
-      f4 x[kSRpw];
-      lds_read4(x, lds0 + static_cast<uint32_t>(slot) * (kSTile * 4) + mine);
-#pragma unroll
-      for (int r = 0; r < kSRpw; ++r) acc[r] += x[r];  // strictly in list order (:25-28)
-      slot = slot + 1 == kSS ? 0 : slot + 1;
-    }
-    f4 m[kSRpw];
-#pragma unroll
-    for (int r = 0; r < kSRpw; ++r) m[r] = div4<RECIP>(acc[r], fk, inv);  // (:31-32)
-    if (tl.out) {
-#pragma unroll
-      for (int r = 0; r < kSRpw; ++r) st(tl.out + o + r * 256, m[r]);
-    }
-    if (tl.w) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w DMA (and its older stores)
-      f4 wq[kSRpw];
-      lds_read4(wq, lds0 + static_cast<uint32_t>(kSS * kSTile * 4) + mine);
-#pragma unroll
-      for (int r = 0; r < kSRpw; ++r) st(tl.w + o + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
+    if (cw == 0 && lane == 0 && atomicAdd(&queue[1], 1) == static_cast<int>(G) - 1) {
+      atomicExch(&queue[0], 0);  // every block has made its last claim: the stream's next launch starts at 0
+      atomicExch(&queue[1], 0);
     }
   }
 }
@@ -512,19 +690,65 @@ static int64_t split_tiles_for(int K, int64_t full) {
 // at 256 x 125M, +2.3% at 16 x 100M.
 static dim3 split_grid(int64_t tiles) { return dim3(static_cast<unsigned>(tiles)); }
 
+// QUEUE launches (see fedavg_split_kernel): one [claims, blocks done] counter
+// pair per (device, stream), allocated and zeroed on the stream's first
+// launch; launches on one stream run in order and each leaves it zeroed.
+#ifndef P2P_SPLIT_QUEUE
+#define P2P_SPLIT_QUEUE 0
+#endif
+static int32_t* queue_counter(hipStream_t st) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, int32_t*> counters;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = counters.find({dev, st});
+  if (it != counters.end()) return it->second;
+  int32_t* q = nullptr;
+  if (hipMalloc(&q, 2 * sizeof(int32_t)) != hipSuccess) return nullptr;
+  if (hipMemset(q, 0, 2 * sizeof(int32_t)) != hipSuccess) {
+    (void)hipFree(q);
+    return nullptr;
+  }
+  counters[{dev, st}] = q;
+  return q;
+}
+
+// The split kernel over ntiles tiles in mode MODE: the tile queue's
+// persistent grid when built with it (K from the kernarg, K >= kQueueMinK),
+// else one block per tile.
+template <int MODE>
+static void launch_split(const float* const* peers, int K, const int32_t* k_dev, int64_t ntiles, float* w,
+                         float* out, float lr, const p2p_split_tile_t* tiles, const Seg* segs,
+                         const p2p_row_chunk_t* chunks, bool recip, hipStream_t st) {
+  const dim3 block(64 * (kSL + kSC));
+  int32_t* q = (P2P_SPLIT_QUEUE && !k_dev && K >= kQueueMinK) ? queue_counter(st) : nullptr;
+  if (q) {
+    const dim3 grid(static_cast<unsigned>(ntiles < device_cus() ? ntiles : device_cus()));
+    if (recip)
+      hipLaunchKernelGGL((fedavg_split_kernel<true, MODE, true>), grid, block, 0, st, peers, K, k_dev, ntiles, w, out,
+                         lr, tiles, segs, chunks, q);
+    else
+      hipLaunchKernelGGL((fedavg_split_kernel<false, MODE, true>), grid, block, 0, st, peers, K, k_dev, ntiles, w,
+                         out, lr, tiles, segs, chunks, q);
+    return;
+  }
+  const dim3 grid = split_grid(ntiles);
+  if (recip)
+    hipLaunchKernelGGL((fedavg_split_kernel<true, MODE, false>), grid, block, 0, st, peers, K, k_dev, ntiles, w, out,
+                       lr, tiles, segs, chunks, nullptr);
+  else
+    hipLaunchKernelGGL((fedavg_split_kernel<false, MODE, false>), grid, block, 0, st, peers, K, k_dev, ntiles, w, out,
+                       lr, tiles, segs, chunks, nullptr);
+}
+
 static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,
                         float lr, hipStream_t stream, bool recip = false) {
   int64_t done = 0;
   {
     const int64_t tiles = split_tiles_for(K, n / kSTile);
     if (tiles > 0) {
-      const dim3 grid = split_grid(tiles), block(64 * (kSL + kSC));
-      if (recip)
-        hipLaunchKernelGGL((fedavg_split_kernel<true, false>), grid, block, 0, stream, peers, K, k_dev, tiles, w, out,
-                           lr, nullptr, nullptr);
-      else
-        hipLaunchKernelGGL((fedavg_split_kernel<false, false>), grid, block, 0, stream, peers, K, k_dev, tiles, w, out,
-                           lr, nullptr, nullptr);
+      launch_split<kFlat>(peers, K, k_dev, tiles, w, out, lr, nullptr, nullptr, nullptr, recip, stream);
       done = tiles * kSTile;
       if (done == n) return;
     }
@@ -583,14 +807,8 @@ extern "C" int32_t p2p_fedavg_split_rows_f32(const float* const* rows, int32_t k
                                             p2p_stream_t stream) {
   if (!rows || !chunks || k < 1 || ntiles < 1) return P2P_ERR_INVALID;
   if (rule != P2P_RULE_FEDAVG && rule != P2P_RULE_FEDAVG_TORCH_GPU) return P2P_ERR_INVALID;
-  const dim3 grid = split_grid(ntiles), block(64 * (kSL + kSC));
-  const hipStream_t st = static_cast<hipStream_t>(stream);
-  if (rule == P2P_RULE_FEDAVG_TORCH_GPU)
-    hipLaunchKernelGGL((fedavg_split_kernel<true, false, true>), grid, block, 0, st, rows, k, nullptr, ntiles, nullptr,
-                       nullptr, lr, nullptr, nullptr, chunks);
-  else
-    hipLaunchKernelGGL((fedavg_split_kernel<false, false, true>), grid, block, 0, st, rows, k, nullptr, ntiles,
-                       nullptr, nullptr, lr, nullptr, nullptr, chunks);
+  launch_split<kRows>(rows, k, nullptr, ntiles, nullptr, nullptr, lr, nullptr, nullptr, chunks,
+                      rule == P2P_RULE_FEDAVG_TORCH_GPU, static_cast<hipStream_t>(stream));
   return launch_status();
 }
 
@@ -600,14 +818,19 @@ extern "C" int32_t p2p_fedavg_split_segments_f32(const p2p_split_tile_t* tiles, 
   if (!tiles || !segs || k < 1 || ntiles < 0) return P2P_ERR_INVALID;
   if (rule != P2P_RULE_FEDAVG && rule != P2P_RULE_FEDAVG_TORCH_GPU) return P2P_ERR_INVALID;
   if (ntiles == 0) return P2P_OK;
-  const dim3 grid = split_grid(ntiles), block(64 * (kSL + kSC));
-  const hipStream_t st = static_cast<hipStream_t>(stream);
-  if (rule == P2P_RULE_FEDAVG_TORCH_GPU)
-    hipLaunchKernelGGL((fedavg_split_kernel<true, true>), grid, block, 0, st, nullptr, k, nullptr, ntiles, nullptr,
-                       nullptr, lr, tiles, segs);
-  else
-    hipLaunchKernelGGL((fedavg_split_kernel<false, true>), grid, block, 0, st, nullptr, k, nullptr, ntiles, nullptr,
-                       nullptr, lr, tiles, segs);
+  launch_split<kSegs>(nullptr, k, nullptr, ntiles, nullptr, nullptr, lr, tiles, segs, nullptr,
+                      rule == P2P_RULE_FEDAVG_TORCH_GPU, static_cast<hipStream_t>(stream));
+  return launch_status();
+}
+
+extern "C" int32_t p2p_fedavg_split_chunks_f32(const p2p_split_tile_t* chunks, int64_t ntiles,
+                                               const p2p_segment_t* segs, int32_t k, int32_t rule, float lr,
+                                               p2p_stream_t stream) {
+  if (!chunks || !segs || k < 1 || ntiles < 0) return P2P_ERR_INVALID;
+  if (rule != P2P_RULE_FEDAVG && rule != P2P_RULE_FEDAVG_TORCH_GPU) return P2P_ERR_INVALID;
+  if (ntiles == 0) return P2P_OK;
+  launch_split<kChunks>(nullptr, k, nullptr, ntiles, nullptr, nullptr, lr, chunks, segs, nullptr,
+                        rule == P2P_RULE_FEDAVG_TORCH_GPU, static_cast<hipStream_t>(stream));
   return launch_status();
 }
 

@@ -307,6 +307,42 @@ def _split_plan(ptrs: np.ndarray, w_ptrs, out_ptrs, n_arr: np.ndarray, K: int, r
     return taken, lst
 
 
+def _chunk_plan(ptrs: np.ndarray, w_ptrs, out_ptrs, n_arr: np.ndarray, K: int, r: int):
+    """FedAvg over a state_dict of separately allocated tensors on the split
+    kernel in one launch (include/p2pdl.h p2p_fedavg_split_chunks_f32): every
+    key whose K peer pointers and w / out are 16-B aligned, cut into
+    1024-element chunks, eight chunks per split tile, the last tile padded
+    (seg -1).  Taken for K >= 16 when the tiles fill at least one round of
+    the CUs (p2p_fedavg_split_plan); below that the VGPR segment kernel's
+    smaller blocks cover the chip better.  Returns (chunked keys mask, the
+    chunk list) or None."""
+    if r not in FEDAVG_RULES or K < 16:
+        return None
+    aligned = (ptrs % np.uint64(16) == 0).all(axis=1) & (np.asarray(w_ptrs, dtype=np.uint64) % np.uint64(16) == 0)
+    if out_ptrs is not None:
+        aligned &= np.asarray(out_ptrs, dtype=np.uint64) % np.uint64(16) == 0
+    aligned &= n_arr > 0
+    nch = np.where(aligned, -(-n_arr // ROW_CHUNK), 0)
+    C = int(nch.sum())
+    ntiles = -(-C // (SPLIT_TILE // ROW_CHUNK))
+    if ntiles == 0 or int(N.lib().p2p_fedavg_split_plan(K, ntiles)) <= 0:
+        return None
+    lst = np.zeros(ntiles * (SPLIT_TILE // ROW_CHUNK), dtype=_SPLIT_DTYPE)
+    lst["seg"][C:] = -1  # padding of the last tile
+    lst["seg"][:C] = np.repeat(np.arange(len(n_arr), dtype=np.int64), nch)
+    lst["c0"][:C] = (np.arange(C, dtype=np.int64) - np.repeat(np.cumsum(nch) - nch, nch)) * ROW_CHUNK
+    return aligned, lst
+
+
+# How a FedAvg state_dict of separately allocated tensors runs: "chunks" (the
+# product: one split launch by 1024-float chunks, _chunk_plan), "tiles"
+# (round 5: whole 8192-float tiles on the split kernel, whole CU rounds,
+# from SPLIT_SEGMENT_MIN_TILES up, the rest on the VGPR kernel) or "vgpr"
+# (the VGPR segment kernel alone).  Same bits on every route; the others are
+# kept for A/B (tools/chunks_ab.py) and their tests.
+STATE_DICT_ROUTE = "chunks"
+
+
 def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_frac, outs, dev, cache_key=None):
     r = rule_id(rule)
     if r not in FEDAVG_RULES and K > MAX_ROBUST_PEERS:
@@ -318,12 +354,23 @@ def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_fra
     w_ptrs = [w.data_ptr() for w in ws]
     out_ptrs = [o.data_ptr() for o in outs] if outs is not None else None
     ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
-    plan = _split_plan(ptrs, w_ptrs, out_ptrs, n_arr, K, r)
+    route = STATE_DICT_ROUTE
+    plan = chunks = None
+    if route == "chunks":
+        chunks = _chunk_plan(ptrs, w_ptrs, out_ptrs, n_arr, K, r)
+    elif route == "tiles":
+        plan = _split_plan(ptrs, w_ptrs, out_ptrs, n_arr, K, r)
+    elif route != "vgpr":
+        raise ValueError(f"unknown STATE_DICT_ROUTE {route!r}")
     # The table the VGPR segment kernel runs: every segment, or -- with a
     # split plan -- what the split kernel leaves of each (its tail past the
     # taken whole tiles), as segments of their own whose peer rows, w and out
-    # start at that offset.
-    if plan is None:
+    # start at that offset; with a chunk plan, the keys it could not take.
+    if chunks is not None:
+        rem_idx = np.nonzero(~chunks[0] & (n_arr > 0))[0]
+        start = np.zeros(len(rem_idx), dtype=np.int64)
+        plan = (None, chunks[1])
+    elif plan is None:
         rem_idx, start = np.arange(L), np.zeros(L, dtype=np.int64)
     else:
         taken = plan[0]
@@ -367,7 +414,12 @@ def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_fra
     host[offs[1]:offs[2]] = rem.view(np.uint8)
     host[offs[4]:offs[5]] = rem_ptrs.view(np.uint8).reshape(-1)
     _RING.to_device(host, dev, out=buf)
-    split = None if plan is None else (int(offs[2]), len(lst), int(offs[0]))
+    if plan is None:
+        split = None
+    elif chunks is not None:  # the chunk list: ntiles * 8 entries
+        split = (int(offs[2]), len(lst) // (SPLIT_TILE // ROW_CHUNK), int(offs[0]), "chunks")
+    else:
+        split = (int(offs[2]), len(lst), int(offs[0]), "tiles")
     entry = (buf, tiles, r, b, torch.cuda.current_stream(dev).cuda_stream, (int(offs[1]), Lr, split))
     with torch.cuda.device(dev):
         _launch_entry(entry, K, lr, N.stream_handle())
@@ -442,9 +494,13 @@ def _launch_entry(entry, K: int, lr: float, stream) -> None:
         return
     rem_off, Lr, split = extra
     if split is not None:
-        lst_off, S, segs_off = split
-        N.check(N.lib().p2p_fedavg_split_segments_f32(base + lst_off, S, base + segs_off, K, r, lr, stream),
-                "p2p_fedavg_split_segments_f32")
+        lst_off, S, segs_off, how = split
+        if how == "chunks":
+            N.check(N.lib().p2p_fedavg_split_chunks_f32(base + lst_off, S, base + segs_off, K, r, lr, stream),
+                    "p2p_fedavg_split_chunks_f32")
+        else:
+            N.check(N.lib().p2p_fedavg_split_segments_f32(base + lst_off, S, base + segs_off, K, r, lr, stream),
+                    "p2p_fedavg_split_segments_f32")
     if tiles:
         _launch_table(base + rem_off, Lr, tiles, K, r, b, lr, stream=stream)
 

@@ -93,3 +93,35 @@ def test_init_process_group_has_a_timeout():
     src = open(bench.__file__).read()
     assert 'init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)' in src
     assert "init_process_group(backend, timeout=tmo)" in src
+
+
+def test_pipeline_summary_fields():
+    """a rank's pipeline record -- overlap fraction
+    (sum kernel + sum gather - wall) / sum gather and the all-gather's
+    algorithm / bus bandwidth per plane -- from per-plane event times."""
+    # two planes of 1M fp32 at N = 2: each all-gather writes 8 MB
+    nbytes = [4 * 1_000_000 * 2] * 2
+    hidden = bench.pipeline_summary(1, [10.0, 10.0], [2.0, 2.0], 22.0, nbytes, 2)
+    assert hidden["rank"] == 1 and hidden["kernel_ms"] == 20.0 and hidden["allgather_ms"] == 4.0
+    assert hidden["overlap_frac"] == 0.5  # (20 + 4 - 22) / 4: the first gather hid, the last did not
+    assert hidden["allgather_algbw_gbs"] == 4.0 and hidden["allgather_busbw_gbs"] == 2.0
+    inline = bench.pipeline_summary(0, [10.0, 10.0], [2.0, 2.0], 24.0, nbytes, 2)
+    assert inline["overlap_frac"] == 0.0
+    assert bench.pipeline_summary(0, [1.0], [], 1.0, [], 1)["overlap_frac"] is None  # one rank: no gather
+    assert "reduction bound" in bench.gather_verdict([dict(hidden, overlap_frac=0.9)])
+    assert "serialised" in bench.gather_verdict([inline])
+    slow = bench.pipeline_summary(0, [10.0, 10.0], [15.0, 15.0], 40.0, nbytes, 2)
+    assert "all-gather bound" in bench.gather_verdict([hidden, slow])
+
+
+def test_gather_switch_parses():
+    import sys as _sys
+
+    saved = _sys.argv
+    try:
+        _sys.argv = ["bench.py", "--gpus", "2", "--gather", "inline"]
+        assert bench.parse().gather == "inline"
+        _sys.argv = ["bench.py"]
+        assert bench.parse().gather == "overlap"
+    finally:
+        _sys.argv = saved

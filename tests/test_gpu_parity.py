@@ -218,6 +218,25 @@ def test_fedavg_split_kernel_vs_oracle(cuda, k, n, rule):
         assert_bits_equal(got_w[a:b], w_ref, what=f"apply [{a}, {b})")
 
 
+def test_split_kernel_repeated_launches_on_two_streams(cuda):
+    """Back-to-back split launches on one stream and interleaved on two
+    (the tile queue's per-stream counter, when the build has it, must start
+    every launch at zero): every mean bit-exact, every launch."""
+    k, n, seed = 16, 2 * 256 * SPLIT_TILE + 77, 0x5B1A
+    rows, _ = split_case(cuda, k, n, seed, pitch_pad=64)
+    want = split_expect(k, seed, 0, n)[1]
+    s1, s2 = torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)
+    outs = []
+    for i in range(6):
+        with torch.cuda.stream(s1 if i % 3 else s2):
+            o = torch.full((n,), float("nan"), dtype=torch.float32, device=cuda)
+            ops.aggregate(rows, "fedavg", out=o)
+            outs.append(o)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        assert_bits_equal(host(o), want, what=f"launch {i}")
+
+
 def test_fedavg_split_kernel_unaligned_rows_and_mean_only(cuda):
     """Rows 4-B but not 16-B aligned: the split kernel's element-wise path,
     same bits; then the mean alone (no w) through the DMA path."""
@@ -257,14 +276,18 @@ def test_fedavg_split_kernel_devk(cuda):
         assert_bits_equal(got[a:b], split_expect(k, seed, a, b)[0], what=f"devk [{a}, {b})")
 
 
+@pytest.mark.parametrize("route", ["chunks", "tiles", "vgpr"])
 @pytest.mark.parametrize("k,rule,with_out", [(20, "fedavg", False), (64, "fedavg_torch_gpu", True)])
-def test_fedavg_split_segments_vs_oracle(cuda, k, rule, with_out, monkeypatch):
-    """A state_dict through the split kernel's tile list (ops._split_plan:
-    whole 8192-element tiles of aligned segments, whole CU rounds) and the
-    VGPR segment kernel over the rest -- segments of every size class, one
-    segment whose peer views are only 4-B aligned (left out of the list) --
-    bit-exact against the oracle, segment by segment."""
+def test_fedavg_split_segments_vs_oracle(cuda, k, rule, with_out, route, monkeypatch):
+    """A state_dict on each route (ops.STATE_DICT_ROUTE): the chunk list
+    (ops._chunk_plan, the product), the split kernel's tile list
+    (ops._split_plan: whole 8192-element tiles of aligned segments, whole CU
+    rounds) and the VGPR segment kernel over the rest, or the VGPR kernel
+    alone -- segments of every size class, one segment whose peer views are
+    only 4-B aligned (left to the VGPR kernel) -- bit-exact against the
+    oracle, segment by segment."""
     monkeypatch.setattr(ops, "SPLIT_SEGMENT_MIN_TILES", 0)  # these sizes sit below the product's gate
+    monkeypatch.setattr(ops, "STATE_DICT_ROUTE", route)
     sizes = [2_500_001, 100, 8191, 8192, 700_001, 1_234_567, 3, 300_000]
     seed = 0x5E65 + k
     ws, peer_lists, outs, want_w, want_o = [], [[] for _ in range(k)], [], [], []
@@ -291,9 +314,11 @@ def test_fedavg_split_segments_vs_oracle(cuda, k, rule, with_out, monkeypatch):
             assert_bits_equal(host(outs[l]), want_o[l], what=f"segment {l} mean")
 
 
-def test_fedavg_split_segments_at_the_product_gate(cuda):
-    """Default gate: a 16-peer state_dict with SPLIT_SEGMENT_MIN_TILES whole
-    tiles and more goes through the split plan, bit-exact on every tensor."""
+def test_fedavg_split_segments_at_the_product_gate(cuda, monkeypatch):
+    """The tiles route's default gate: a 16-peer state_dict with
+    SPLIT_SEGMENT_MIN_TILES whole tiles and more goes through the split plan,
+    bit-exact on every tensor."""
+    monkeypatch.setattr(ops, "STATE_DICT_ROUTE", "tiles")
     k, rule, seed = 16, "fedavg", 0x5E70
     sizes = [9_000_001, 8_200_000 + 5, 100]
     plan_tiles = sum(n // SPLIT_TILE for n in sizes)
@@ -311,6 +336,147 @@ def test_fedavg_split_segments_at_the_product_gate(cuda):
     ops.aggregate_segments_(ws, peer_lists, rule)
     for l in range(len(sizes)):
         assert_bits_equal(host(ws[l]), want[l], what=f"segment {l} w")
+
+
+# Keys of a state_dict as pickle.loads hands them to the reference's listener
+# (node/node.py:138-141): every tensor its own allocation.  Ragged ends of
+# every kind: n % 4 in {1, 2, 3} (the float4 that straddles a key's end),
+# keys shorter than one float4 and one chunk, exactly one chunk, and 2,190
+# chunks in all (274 split tiles: more than one round of 256 CUs).
+CHUNK_SIZES = [1_234_567, 1, 2, 3, 5, 1023, 1024, 1025, 4097, 8191, 300_001, 9 * 64 * 9, 700_000, 100, 6]
+
+
+def _chunk_case(dev, k, sizes, seed, misaligned=(), nan_tail=False):
+    """Separately allocated peer tensors per key (a misaligned key's views
+    start one float into their allocation; nan_tail: 4 NaN floats follow each
+    view inside its allocation) and separately allocated model tensors;
+    returns (ws, peer_lists, host peers per key, host w per key)."""
+    ws, peer_lists, hp, hw = [], [[] for _ in range(k)], [], []
+    for l, n in enumerate(sizes):
+        keyp = []
+        for p in range(k):
+            o = 1 if l in misaligned else 0
+            if nan_tail:
+                raw = torch.full((o + n + 4,), float("nan"), dtype=torch.float32, device=dev)
+            else:
+                raw = torch.empty(o + n, dtype=torch.float32, device=dev)
+            v = raw[o:o + n]
+            ops.fill_synthetic_(v, seed + l, p, 1e-2)
+            peer_lists[p].append(v)
+            keyp.append(host(v))
+        w = torch.empty(n, dtype=torch.float32, device=dev)
+        ops.fill_synthetic_(w, seed + l, 0xFFFFF, 5e-2)
+        ws.append(w)
+        hp.append(keyp)
+        hw.append(host(w))
+    return ws, peer_lists, hp, hw
+
+
+@pytest.mark.parametrize("k,rule,with_out", [(16, "fedavg", True), (17, "fedavg", False),
+                                             (64, "fedavg_torch_gpu", False), (20, "fedavg_torch_gpu", True)])
+def test_fedavg_chunks_separate_tensors_vs_oracle(cuda, k, rule, with_out, monkeypatch):
+    """a state_dict of separately allocated tensors on
+    the split kernel's chunk list (p2p_fedavg_split_chunks_f32), ONE launch
+    (no VGPR remainder: every key is aligned), bit-exact per key against the
+    oracle -- ragged key ends, keys shorter than a float4, padding chunks of
+    the last tile -- with and without the mean output."""
+    seed = 0xC4 + k
+    ws, peer_lists, hp, hw = _chunk_case(cuda, k, CHUNK_SIZES, seed)
+    outs = [torch.full_like(w, float("nan")) for w in ws] if with_out else None
+    launches = []
+    lib = ops.N.lib()
+    for name in ("p2p_fedavg_split_chunks_f32", "p2p_aggregate_segments_f32", "p2p_fedavg_split_segments_f32"):
+        real = getattr(lib, name)
+        monkeypatch.setattr(lib, name, lambda *a, _r=real, _n=name: (launches.append(_n), _r(*a))[1])
+    ops.aggregate_segments_(ws, peer_lists, rule, outs=outs)
+    assert launches == ["p2p_fedavg_split_chunks_f32"]
+    for l in range(len(CHUNK_SIZES)):
+        wr, orr = oracle.fedavg(hp[l], hw[l], want_out=True, torch_gpu=rule == "fedavg_torch_gpu")
+        assert_bits_equal(host(ws[l]), wr, what=f"key {l} (n={CHUNK_SIZES[l]}) w")
+        if with_out:
+            assert_bits_equal(host(outs[l]), orr, what=f"key {l} (n={CHUNK_SIZES[l]}) mean")
+
+
+def test_fedavg_chunks_misaligned_key_and_guard_bytes(cuda, monkeypatch):
+    """A key whose peer views are only 4-B aligned goes to the VGPR kernel
+    beside the chunk launch; no read and no write leaves a key: the float
+    after each model tensor's end (inside its allocation) is unchanged and
+    the peers' floats past their views' ends (NaN) never reach a result."""
+    k, seed = 16, 0xC5
+    sizes = CHUNK_SIZES
+    ws, peer_lists, hp, hw = _chunk_case(cuda, k, sizes, seed, misaligned=(10,), nan_tail=True)
+    # model tensors as views of allocations one float4 longer, guard = 7.0
+    guarded = []
+    for l, w in enumerate(ws):
+        raw = torch.full((w.numel() + 4,), 7.0, dtype=torch.float32, device=cuda)
+        raw[:w.numel()].copy_(w)
+        guarded.append(raw)
+        ws[l] = raw[:w.numel()]
+    launches = []
+    lib = ops.N.lib()
+    for name in ("p2p_fedavg_split_chunks_f32", "p2p_aggregate_segments_f32"):
+        real = getattr(lib, name)
+        monkeypatch.setattr(lib, name, lambda *a, _r=real, _n=name: (launches.append(_n), _r(*a))[1])
+    ops.aggregate_segments_(ws, peer_lists, "fedavg")
+    assert launches == ["p2p_fedavg_split_chunks_f32", "p2p_aggregate_segments_f32"]
+    for l in range(len(sizes)):
+        wr, _ = oracle.fedavg(hp[l], hw[l])
+        assert_bits_equal(host(ws[l]), wr, what=f"key {l} w")
+        assert (host(guarded[l][sizes[l]:]) == 7.0).all(), f"key {l}: wrote past the tensor's end"
+
+
+def test_fedavg_chunks_through_pickle_loads(cuda, monkeypatch):
+    """The reference's own receive path: each update pickled and unpickled
+    (node/node.py:285 dumps, :138 loads), so every tensor of every update is
+    its own allocation, then the drop-in aggregate_models (general path: the
+    C-gathered peer table) -- on the chunk launch, bit-exact; again at the
+    same addresses through the cached table."""
+    from p2pdl_amd.aggregator import aggregation as agg
+
+    monkeypatch.setattr(agg, "broadcast_global_model_update", lambda self: None)
+    k, seed = 16, 0xC6
+    shapes = [(f"k{i}", (n,)) for i, n in enumerate(CHUNK_SIZES)]
+    n = sum(CHUNK_SIZES)
+    peers = [oracle.synth(n, seed, p, 1e-2) for p in range(k)]
+    w0 = oracle.synth(n, seed, 0xFFFFF, 5e-2)
+    want, _ = oracle.fedavg(peers, w0)
+    want2, _ = oracle.fedavg(peers, want)
+    upd = [pickle.loads(pickle.dumps(split(p, shapes, cuda))) for p in peers]
+    assert all(t.is_cuda for t in upd[0].values())
+    model = Holder(shapes).to(cuda)
+    with torch.no_grad():
+        model.load_state_dict(split(w0, shapes, cuda))
+    launches = []
+    lib = ops.N.lib()
+    for name in ("p2p_fedavg_split_chunks_f32", "p2p_aggregate_segments_f32"):
+        real = getattr(lib, name)
+        monkeypatch.setattr(lib, name, lambda *a, _r=real, _n=name: (launches.append(_n), _r(*a))[1])
+    agg.aggregate_models(fake_node(model, upd))
+    got = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+    assert_bits_equal(got, want, what="pickle.loads updates, round 1")
+    agg.aggregate_models(fake_node(model, upd))
+    got = np.concatenate([host(t).reshape(-1) for t in model.state_dict().values()])
+    assert_bits_equal(got, want2, what="pickle.loads updates, round 2 (cached table)")
+    assert launches == ["p2p_fedavg_split_chunks_f32"] * 2
+
+
+def test_chunk_plan_host_logic(cuda):
+    """The chunk list itself: aligned keys only, 1024-element chunks in key
+    order, c0 per chunk, the last tile padded with seg -1; K < 16, robust
+    rules and fewer tiles than CUs decline."""
+    K, cus = 16, torch.cuda.get_device_properties(cuda).multi_processor_count
+    n_arr = np.array([3000, 8 * 1024 * cus, 5, 2048], dtype=np.int64)
+    ptrs = np.full((4, K), 1 << 20, dtype=np.uint64)
+    ptrs[3, 2] += 4  # key 3: one peer view 4-B aligned only
+    mask, lst = ops._chunk_plan(ptrs, [1 << 24] * 4, None, n_arr, K, 0)
+    assert list(mask) == [True, True, True, False]
+    C = 3 + 8 * cus + 1
+    assert len(lst) == 8 * -(-C // 8)
+    assert list(lst["seg"][:4]) == [0, 0, 0, 1] and list(lst["c0"][:4]) == [0, 1024, 2048, 0]
+    assert lst["seg"][C - 1] == 2 and lst["c0"][C - 1] == 0 and (lst["seg"][C:] == -1).all()
+    assert ops._chunk_plan(ptrs, [1 << 24] * 4, None, n_arr, 15, 0) is None
+    assert ops._chunk_plan(ptrs, [1 << 24] * 4, None, n_arr, K, 1) is None
+    assert ops._chunk_plan(ptrs, [1 << 24] * 4, None, n_arr[:1], K, 0) is None  # 3 chunks: below a round
 
 
 ROWS_SIZES = [2_300_001, 100, 1023, 1024, 1025, 9 * 64 * 9, 300_001, 3, 4096, 8191]

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round 6: the split kernel's tile queue (P2P_SPLIT_QUEUE,
+# tools/libp2pdl_queue.so from tools/variants/queue.py) against the product
+# library, alternating processes on one box, on bench shapes: "<name>|<bench args>".
+#   usage: tools/queue_ab.sh <out-dir> <rounds> "<name>|<args>" ...
+set -o pipefail
+OUT=$1; R=$2; shift 2
+mkdir -p "$OUT"
+B="bench.py --no-sub --no-cpu-baseline --no-reference-gpu --steps 10 --warmup 2"
+for i in $(seq 1 "$R"); do
+  for spec in "$@"; do
+    name=${spec%%|*}; args=${spec#*|}
+    for lib in queue prod; do
+      if [ $lib = prod ]; then L=""; else L="P2P_LIB=tools/libp2pdl_$lib.so"; fi
+      env $L timeout -k 10 240 python3 -u $B $args > "$OUT/${lib}_${name}_$i.json" 2> "$OUT/${lib}_${name}_$i.err" \
+        || { tail "$OUT/${lib}_${name}_$i.err"; exit 1; }
+    done
+  done
+done
+python3 - "$OUT" <<'PY'
+import glob, json, os, sys
+rows = {}
+for f in sorted(glob.glob(os.path.join(sys.argv[1], "*.json"))):
+    for line in open(f):
+        if line.startswith("{"):
+            d = json.loads(line)
+            who, rest = os.path.basename(f)[:-5].split("_", 1)
+            name = rest.rsplit("_", 1)[0]
+            r = d["roofline"]
+            rows.setdefault((name, who), []).append((r["frac"], r.get("kernel_ms")))
+for (name, who), v in sorted(rows.items()):
+    print(f"{name:14s} {who:6s} " + "  ".join(f"{f:.4f} ({k} ms)" for f, k in v))
+PY
