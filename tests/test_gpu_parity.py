@@ -404,7 +404,7 @@ def test_fedavg_chunks_misaligned_key_and_guard_bytes(cuda, monkeypatch):
     the peers' floats past their views' ends (NaN) never reach a result."""
     k, seed = 16, 0xC5
     sizes = CHUNK_SIZES
-    ws, peer_lists, hp, hw = _chunk_case(cuda, k, sizes, seed, misaligned=(10,), nan_tail=True)
+    ws, peer_lists, hp, hw = _chunk_case(cuda, k, sizes, seed, misaligned=(13,), nan_tail=True)
     # model tensors as views of allocations one float4 longer, guard = 7.0
     guarded = []
     for l, w in enumerate(ws):
