@@ -1814,6 +1814,8 @@ def main():
             "config": main_rec["config"], "roofline": main_rec["roofline"],
             "cpu_baseline": main_rec.get("cpu_baseline"),
         }
+        if main_rec.get("general_path"):
+            line["general_path"] = main_rec["general_path"]
         if sub:
             line["sub"] = {k: compact_sub(v) for k, v in sub.items()}
         print(json.dumps(line), flush=True)

@@ -25,8 +25,6 @@
 // 6.2-6.4 TB/s = 78-80% of 8 TB/s.  No inter-block reuse exists, so no XCD
 // remap is needed (guide T1: 0% on elementwise).
 #include <atomic>
-#include <map>
-#include <mutex>
 
 #include "p2p_common.h"
 
@@ -500,8 +498,8 @@ __device__ __forceinline__ void flat_tile(const SplitTile& tl, int K, int lane, 
 enum SplitMode { kFlat = 0, kSegs = 1, kRows = 2, kChunks = 3 };
 
 // QUEUE (round 6, tools/split_fixed_lab.hip variant Q): a persistent grid
-// of min(tiles, CUs) blocks that claim their tiles from a per-stream counter
-// (`queue`: [claims, blocks done], zero at launch start) instead of one
+// of min(tiles, CUs) blocks that claim their tiles from a counter pair of
+// g_tile_queue ([claims, blocks done], zero at launch start) instead of one
 // block per tile.  A block's loaders then stream tile j+1's first stages
 // during tile j's epilogue (w DMA wait, / K, apply, stores), which a
 // one-tile block leaves the CU idle for.  Consumer wave 0 claims the next
@@ -513,6 +511,8 @@ enum SplitMode { kFlat = 0, kSegs = 1, kRows = 2, kChunks = 3 };
 // finish zeroes the counter for the stream's next launch.
 constexpr int kQW = 2, kQR = 4;
 constexpr int kQueueMinK = kQR + kSS;  // K the queue's publication schedule needs
+constexpr int kQueueSlots = 4096;      // counter pairs, one per launch in flight (see launch_split)
+__device__ int32_t g_tile_queue[2 * kQueueSlots];
 
 template <bool RECIP, int MODE, bool QUEUE = false>
 __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const float* const* __restrict__ peers,
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
                                                                         float lr, const p2p_split_tile_t* tiles,
                                                                         const Seg* segs,
                                                                         const p2p_row_chunk_t* chunks = nullptr,
-                                                                        int32_t* queue = nullptr) {
+                                                                        int queue_slot = -1) {
   constexpr bool SEGS = MODE == kSegs;
   __shared__ __attribute__((aligned(16))) float lds[(kSS + 1) * kSTile];
   __shared__ int64_t tq[4];
@@ -602,6 +602,7 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
     for (int64_t t = b; t < ntiles; t += G) tile(t, [](int) {});
     return;
   } else {
+    int32_t* queue = g_tile_queue + 2 * queue_slot;
     int64_t t = b;
     for (int j = 0;; ++j) {
       int64_t claim = 0;
@@ -690,40 +691,27 @@ static int64_t split_tiles_for(int K, int64_t full) {
 // at 256 x 125M, +2.3% at 16 x 100M.
 static dim3 split_grid(int64_t tiles) { return dim3(static_cast<unsigned>(tiles)); }
 
-// QUEUE launches (see fedavg_split_kernel): one [claims, blocks done] counter
-// pair per (device, stream), allocated and zeroed on the stream's first
-// launch; launches on one stream run in order and each leaves it zeroed.
+// QUEUE launches (see fedavg_split_kernel): launch i takes counter pair
+// i mod kQueueSlots of g_tile_queue (zero at module load; each launch leaves
+// its pair zeroed when its last block ends).  Nothing is allocated and no
+// per-stream state kept, so the call stays graph-capturable (a captured
+// launch keeps its pair: its replays on one stream run in order).  A pair is
+// reused kQueueSlots launches later: the bound is that many split launches
+// in flight at once on one device.
 #ifndef P2P_SPLIT_QUEUE
 #define P2P_SPLIT_QUEUE 0
 #endif
-static int32_t* queue_counter(hipStream_t st) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, int32_t*> counters;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = counters.find({dev, st});
-  if (it != counters.end()) return it->second;
-  int32_t* q = nullptr;
-  if (hipMalloc(&q, 2 * sizeof(int32_t)) != hipSuccess) return nullptr;
-  if (hipMemset(q, 0, 2 * sizeof(int32_t)) != hipSuccess) {
-    (void)hipFree(q);
-    return nullptr;
-  }
-  counters[{dev, st}] = q;
-  return q;
-}
-
+static std::atomic<uint32_t> g_queue_next{0};
 // The split kernel over ntiles tiles in mode MODE: the tile queue's
-// persistent grid when built with it (K from the kernarg, K >= kQueueMinK),
-// else one block per tile.
+// persistent grid of min(tiles, CUs) blocks when built with it (K from the
+// kernarg, K >= kQueueMinK), else one block per tile.
 template <int MODE>
 static void launch_split(const float* const* peers, int K, const int32_t* k_dev, int64_t ntiles, float* w,
                          float* out, float lr, const p2p_split_tile_t* tiles, const Seg* segs,
                          const p2p_row_chunk_t* chunks, bool recip, hipStream_t st) {
   const dim3 block(64 * (kSL + kSC));
-  int32_t* q = (P2P_SPLIT_QUEUE && !k_dev && K >= kQueueMinK) ? queue_counter(st) : nullptr;
-  if (q) {
+  if (P2P_SPLIT_QUEUE && !k_dev && K >= kQueueMinK) {
+    const int q = static_cast<int>(g_queue_next.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
     const dim3 grid(static_cast<unsigned>(ntiles < device_cus() ? ntiles : device_cus()));
     if (recip)
       hipLaunchKernelGGL((fedavg_split_kernel<true, MODE, true>), grid, block, 0, st, peers, K, k_dev, ntiles, w, out,
@@ -736,10 +724,10 @@ static void launch_split(const float* const* peers, int K, const int32_t* k_dev,
   const dim3 grid = split_grid(ntiles);
   if (recip)
     hipLaunchKernelGGL((fedavg_split_kernel<true, MODE, false>), grid, block, 0, st, peers, K, k_dev, ntiles, w, out,
-                       lr, tiles, segs, chunks, nullptr);
+                       lr, tiles, segs, chunks, -1);
   else
     hipLaunchKernelGGL((fedavg_split_kernel<false, MODE, false>), grid, block, 0, st, peers, K, k_dev, ntiles, w, out,
-                       lr, tiles, segs, chunks, nullptr);
+                       lr, tiles, segs, chunks, -1);
 }
 
 static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,

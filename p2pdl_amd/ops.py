@@ -19,6 +19,9 @@ import torch
 from . import _native as N
 from ._native import P2P_RULE_FEDAVG, P2P_RULE_FEDAVG_TORCH_GPU, P2P_RULE_MEDIAN, P2P_RULE_TRIMMED
 
+# the chunk list's C fill (csrc/host_tables.cpp); no silent fallback when it is not built
+_host_tables = N.host_extension("_host_tables")
+
 # 'fedavg': the reference's ops as torch runs them on CPU tensors (true
 # division by K; the golden vectors).  'fedavg_torch_gpu': the same ops as
 # torch runs them on GPU tensors -- the reference's deployment, model on cuda
@@ -318,19 +321,19 @@ def _chunk_plan(ptrs: np.ndarray, w_ptrs, out_ptrs, n_arr: np.ndarray, K: int, r
     chunk list) or None."""
     if r not in FEDAVG_RULES or K < 16:
         return None
-    aligned = (ptrs % np.uint64(16) == 0).all(axis=1) & (np.asarray(w_ptrs, dtype=np.uint64) % np.uint64(16) == 0)
+    low = np.bitwise_or.reduce(ptrs, axis=1) | np.asarray(w_ptrs, dtype=np.uint64)
     if out_ptrs is not None:
-        aligned &= np.asarray(out_ptrs, dtype=np.uint64) % np.uint64(16) == 0
-    aligned &= n_arr > 0
+        low |= np.asarray(out_ptrs, dtype=np.uint64)
+    aligned = ((low & np.uint64(15)) == 0) & (n_arr > 0)
     nch = np.where(aligned, -(-n_arr // ROW_CHUNK), 0)
     C = int(nch.sum())
     ntiles = -(-C // (SPLIT_TILE // ROW_CHUNK))
     if ntiles == 0 or int(N.lib().p2p_fedavg_split_plan(K, ntiles)) <= 0:
         return None
-    lst = np.zeros(ntiles * (SPLIT_TILE // ROW_CHUNK), dtype=_SPLIT_DTYPE)
-    lst["seg"][C:] = -1  # padding of the last tile
-    lst["seg"][:C] = np.repeat(np.arange(len(n_arr), dtype=np.int64), nch)
-    lst["c0"][:C] = (np.arange(C, dtype=np.int64) - np.repeat(np.cumsum(nch) - nch, nch)) * ROW_CHUNK
+    M = ntiles * (SPLIT_TILE // ROW_CHUNK)
+    lst = np.empty(M, dtype=_SPLIT_DTYPE)  # (seg, c0) == p2p_split_tile_t, padded with (-1, 0)
+    if _host_tables.fill_chunk_list(np.ascontiguousarray(nch, dtype=np.int64), lst) != C:
+        raise RuntimeError("chunk list: size mismatch")
     return aligned, lst
 
 

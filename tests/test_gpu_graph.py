@@ -100,3 +100,47 @@ def test_delta_graph_replay(cuda):
     g.replay()
     torch.cuda.synchronize()
     assert not delta.cpu().numpy().view(np.uint32).any()  # x - x = +0 for every finite x
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("route", ["flat", "chunks"])
+def test_split_kernel_graph_replay(cuda, route):
+    """The LDS-DMA split kernel captured and replayed (K = 16, more than one
+    round of tiles): a flat buffer, and a state_dict of separately allocated
+    tensors on the chunk list (its device table built before the capture).
+    A build with the tile queue keeps one counter pair per captured launch,
+    so the replays run in order on it."""
+    from p2pdl_amd import ops
+
+    k = 16
+    sizes = [256 * 8192 + 4099] if route == "flat" else [1_234_567, 5, 1_000_003]
+    peers = [[oracle.synth(n, 41 + i, p, 1e-2) for i, n in enumerate(sizes)] for p in range(k)]
+    w0 = [oracle.synth(n, 41 + i, 0xFFFFF, 5e-2) for i, n in enumerate(sizes)]
+    pd = [[_dev(a, cuda) for a in row] for row in peers]
+    ws = [_dev(a, cuda) for a in w0]
+    if route == "flat":
+        table = ops.pointer_table([row[0] for row in pd], cuda)
+        run = lambda: ops.aggregate(None, "fedavg", w=ws[0], lr=0.1, table=table)  # noqa: E731
+    else:
+        ptrs = np.array([[row[i].data_ptr() for row in pd] for i in range(len(sizes))], dtype=np.uint64)
+        ops.aggregate_ptr_table_(ws, ptrs, "fedavg")  # builds and caches the device table
+        entry = next(reversed(ops._TABLES.values()))
+        assert entry[5][2][3] == "chunks"
+        run = lambda: ops._launch_entry(entry, k, 0.1, ops.N.stream_handle())  # noqa: E731
+    run()  # warm-up
+    torch.cuda.synchronize()
+    for w, a in zip(ws, w0):
+        w.copy_(_dev(a, cuda))
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(cuda)
+    s.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            run()
+    want = list(w0)
+    for _ in range(3):
+        g.replay()
+        want = [oracle.fedavg([row[i] for row in peers], want[i])[0] for i in range(len(sizes))]
+    torch.cuda.synchronize()
+    for w, a in zip(ws, want):
+        assert np.array_equal(w.cpu().numpy().view(np.uint32), a.view(np.uint32))

@@ -28,6 +28,12 @@ for f in sorted(glob.glob(os.path.join(sys.argv[1], "*.json"))):
             name = rest.rsplit("_", 1)[0]
             r = d["roofline"]
             rows.setdefault((name, who), []).append((r["frac"], r.get("kernel_ms")))
+            for s, rec in (d.get("sub") or {}).items():  # e.g. cfg3_full
+                if rec.get("frac") is not None:
+                    rows.setdefault((f"{name}.{s}", who), []).append((rec["frac"], rec.get("kernel_ms")))
+            gp = d.get("general_path") or (d.get("config") or {}).get("general_path")
+            if gp:
+                rows.setdefault((name + ".general", who), []).append((gp["frac_of_hbm_peak"], gp["kernel_ms"]))
 for (name, who), v in sorted(rows.items()):
     print(f"{name:14s} {who:6s} " + "  ".join(f"{f:.4f} ({k} ms)" for f, k in v))
 PY
