@@ -10,7 +10,7 @@ timeout -k 10 400 $T -k "$K" > $O/tests_prod.log 2>&1 || { tail -30 $O/tests_pro
 tail -1 $O/tests_prod.log
 P2P_LIB=tools/libp2pdl_queue.so timeout -k 10 400 $T -k "$K" > $O/tests_queue.log 2>&1 || { tail -30 $O/tests_queue.log; exit 1; }
 tail -1 $O/tests_queue.log
-timeout -k 10 1000 tools/queue_ab.sh $O/ab 3 "cfg3|--workload cfg3" "full|--job cfg3-full --steps 1" "cfg2|--workload cfg2-dropin" \
+timeout -k 10 780 tools/queue_ab.sh $O/ab 3 "cfg3|--workload cfg3" "full|--job cfg3-full --steps 1" "cfg2|--workload cfg2-dropin" \
   "k16n100m|--workload cfg3 --peers 16 --coords 100007936" > $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 1; }
 cat $O/ab.log
 P2P_LIB=tools/libp2pdl_queue.so timeout -k 10 300 python -u tools/chunks_ab.py 15 64:1 16:1 > $O/chunks_ab_queue.log 2>&1 || { tail -30 $O/chunks_ab_queue.log; exit 1; }
