@@ -698,9 +698,18 @@ static dim3 split_grid(int64_t tiles) { return dim3(static_cast<unsigned>(tiles)
 // launch keeps its pair: its replays on one stream run in order).  A pair is
 // reused kQueueSlots launches later: the bound is that many split launches
 // in flight at once on one device.
+// Which launches take the queue (same-box A/Bs, alternating processes,
+// profiles/r06/queue_ab): flat buffers -- the cfg3 planes +2.8-5.1%, the
+// full job +0.4-2.7%, 16 x 100M +5.7% -- and segment / chunk lists (the
+// drop-in's general path, within +-0.5%); not the rows kernel (cfg2 landed
+// -0.4 to -1.0%).  An A/B build may set P2P_SPLIT_QUEUE 0 (no queue at all).
 #ifndef P2P_SPLIT_QUEUE
-#define P2P_SPLIT_QUEUE 0
+#define P2P_SPLIT_QUEUE 1
 #endif
+template <int MODE>
+constexpr bool queue_mode() {
+  return P2P_SPLIT_QUEUE && MODE != kRows;
+}
 static std::atomic<uint32_t> g_queue_next{0};
 // The split kernel over ntiles tiles in mode MODE: the tile queue's
 // persistent grid of min(tiles, CUs) blocks when built with it (K from the
@@ -710,7 +719,7 @@ static void launch_split(const float* const* peers, int K, const int32_t* k_dev,
                          float* out, float lr, const p2p_split_tile_t* tiles, const Seg* segs,
                          const p2p_row_chunk_t* chunks, bool recip, hipStream_t st) {
   const dim3 block(64 * (kSL + kSC));
-  if (P2P_SPLIT_QUEUE && !k_dev && K >= kQueueMinK) {
+  if (queue_mode<MODE>() && !k_dev && K >= kQueueMinK) {
     const int q = static_cast<int>(g_queue_next.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
     const dim3 grid(static_cast<unsigned>(ntiles < device_cus() ? ntiles : device_cus()));
     if (recip)

@@ -1,8 +1,10 @@
 #!/bin/bash
-# Round 6: the split kernel's tile queue (P2P_SPLIT_QUEUE,
-# tools/libp2pdl_queue.so from tools/variants/queue.py) against the product
-# library, alternating processes on one box, on bench shapes: "<name>|<bench args>".
-#   usage: tools/queue_ab.sh <out-dir> <rounds> "<name>|<args>" ...
+# Round 6: the product library against another build
+# (OTHER, default noqueue: tools/libp2pdl_noqueue.so from
+# tools/variants/noqueue.py, the split kernel without its tile queue),
+# alternating processes on one box, on bench shapes: "<name>|<bench args>".
+# (The round's first A/Bs ran the queue as the variant: "queue" vs "prod".)
+#   usage: [OTHER=tag] tools/queue_ab.sh <out-dir> <rounds> "<name>|<args>" ...
 set -o pipefail
 OUT=$1; R=$2; shift 2
 mkdir -p "$OUT"
@@ -10,7 +12,7 @@ B="bench.py --no-sub --no-cpu-baseline --no-reference-gpu --steps 10 --warmup 2"
 for i in $(seq 1 "$R"); do
   for spec in "$@"; do
     name=${spec%%|*}; args=${spec#*|}
-    for lib in queue prod; do
+    for lib in ${OTHER:-noqueue} prod; do
       if [ $lib = prod ]; then L=""; else L="P2P_LIB=tools/libp2pdl_$lib.so"; fi
       env $L timeout -k 10 240 python3 -u $B $args > "$OUT/${lib}_${name}_$i.json" 2> "$OUT/${lib}_${name}_$i.err" \
         || { tail "$OUT/${lib}_${name}_$i.err"; exit 1; }
