@@ -44,8 +44,10 @@ extern "C" {
  * 7: adds p2p_fedavg_split_rows_f32 / p2p_row_chunk_t (a state_dict slab's
  *    rows as flat peers, the model scattered by 1024-float chunks).
  * 8: adds p2p_fedavg_split_chunks_f32 (a state_dict of separately allocated
- *    tensors on the split kernel, one launch, by 1024-float chunks). */
-#define P2P_ABI_VERSION 8
+ *    tensors on the split kernel, one launch, by 1024-float chunks).
+ * 9: adds p2p_aggregate_ex_f32 and P2P_HINT_SHARE_CUS (the FedAvg split
+ *    kernel's tile queue vs a kernel running beside it). */
+#define P2P_ABI_VERSION 9
 
 typedef void *p2p_stream_t; /* hipStream_t */
 
@@ -89,9 +91,12 @@ int64_t p2p_tile_elems(int32_t rule, int32_t k);
  *   acc /= K (:31-32); w += fp32(lr) * acc (:36-38, lr = 0.1 there).
  * Kernel choice (a pure function of k and n, same bits either way): for
  * k >= 16, whole rounds of 8192-float tiles (a multiple of the CU count) run
- * on the LDS-DMA split kernel (loader + consumer waves), the rest on the
- * VGPR kernel.  The peer pointers are read from device memory each launch;
- * 4-byte-aligned (not 16-byte) pointers are handled, more slowly. */
+ * on the LDS-DMA split kernel (loader + consumer waves; a persistent grid of
+ * one block per CU claiming tiles from a counter pair of a device-global
+ * ring, which each launch leaves zeroed -- see p2p_aggregate_ex_f32 for the
+ * one-block-per-tile form), the rest on the VGPR kernel.  The peer pointers
+ * are read from device memory each launch; 4-byte-aligned (not 16-byte)
+ * pointers are handled, more slowly. */
 int32_t p2p_fedavg_apply_f32(const float *const *peers, int32_t k, int64_t n, float *w, float lr,
                              p2p_stream_t stream);
 /* Same reduction, writes acc/K to out (the :15-32 part, no apply). */
@@ -121,6 +126,18 @@ int32_t p2p_trimmed_mean_f32(const float *const *peers, int32_t k, int64_t n, in
  * w, out must be non-null).  trim_b is read only for P2P_RULE_TRIMMED. */
 int32_t p2p_aggregate_f32(const float *const *peers, int32_t k, int64_t n, int32_t rule,
                           int32_t trim_b, float lr, float *w, float *out, p2p_stream_t stream);
+
+/* p2p_aggregate_f32 with launch hints (0 = p2p_aggregate_f32).
+ * P2P_HINT_SHARE_CUS: another kernel runs beside this call on another stream
+ * -- the all-gather of a sharded round (p2pdl_amd/sharded.py PeerPlanes,
+ * SURVEY.md §8(e)).  The FedAvg split kernel then runs one block per tile,
+ * so each tile's end frees a CU the dispatcher can hand to that kernel,
+ * instead of its persistent tile-queue grid, which holds every CU until the
+ * launch ends.  Same results either way; unknown hint bits are
+ * P2P_ERR_INVALID. */
+#define P2P_HINT_SHARE_CUS 1
+int32_t p2p_aggregate_ex_f32(const float *const *peers, int32_t k, int64_t n, int32_t rule, int32_t trim_b,
+                             float lr, float *w, float *out, int32_t hints, p2p_stream_t stream);
 
 /* The LDS-DMA split kernel over whole P2P_SPLIT_TILE-element tiles of a
  * segment table (FedAvg rules only): entry t of the DEVICE array `tiles`

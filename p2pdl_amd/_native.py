@@ -13,16 +13,17 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # P2P_LIB selects a diagnostic build (csrc/Makefile `diag`); default: the product library
 LIB_PATH = os.environ.get("P2P_LIB") or os.path.join(_HERE, "libp2pdl_hip.so")
-ABI_VERSION = 8  # include/p2pdl.h P2P_ABI_VERSION
+ABI_VERSION = 9  # include/p2pdl.h P2P_ABI_VERSION
 
 P2P_RULE_FEDAVG, P2P_RULE_MEDIAN, P2P_RULE_TRIMMED, P2P_RULE_FEDAVG_TORCH_GPU = 0, 1, 2, 3
 P2P_DTYPE_F16, P2P_DTYPE_BF16 = 1, 2
+P2P_HINT_SHARE_CUS = 1  # include/p2pdl.h (ABI 9)
 
 # Every symbol include/p2pdl.h declares (tests check the .so exports them).
 EXPORTS = (
     "p2p_abi_version", "p2p_strerror", "p2p_tile_elems",
     "p2p_fedavg_apply_f32", "p2p_mean_f32", "p2p_fedavg_apply_devk_f32", "p2p_fedavg_apply_16",
-    "p2p_median_f32", "p2p_trimmed_mean_f32", "p2p_aggregate_f32",
+    "p2p_median_f32", "p2p_trimmed_mean_f32", "p2p_aggregate_f32", "p2p_aggregate_ex_f32",
     "p2p_aggregate_segments_f32", "p2p_fedavg_split_plan", "p2p_fedavg_split_segments_f32",
     "p2p_fedavg_split_rows_f32", "p2p_fedavg_split_chunks_f32", "p2p_apply_f32",
     "p2p_sha256_batch", "p2p_digest_accept", "p2p_fill_synthetic_f32",
@@ -71,6 +72,7 @@ _SIGS = {
     "p2p_median_f32": ([_P, _I32, _I64, _P, _P], _I32),
     "p2p_trimmed_mean_f32": ([_P, _I32, _I64, _I32, _P, _P], _I32),
     "p2p_aggregate_f32": ([_P, _I32, _I64, _I32, _I32, _F32, _P, _P, _P], _I32),
+    "p2p_aggregate_ex_f32": ([_P, _I32, _I64, _I32, _I32, _F32, _P, _P, _I32, _P], _I32),
     "p2p_aggregate_segments_f32": ([_P, _I32, _I64, _I32, _I32, _I32, _F32, _P], _I32),
     "p2p_fedavg_split_plan": ([_I32, _I64], _I64),
     "p2p_fedavg_split_segments_f32": ([_P, _I64, _P, _I32, _I32, _F32, _P], _I32),

@@ -12,7 +12,7 @@ extern "C" int32_t p2p_robust_dispatch(const float* const* peers, const p2p_segm
                                        p2p_stream_t stream);
 
 int32_t p2p_fedavg_flat_launch(const float* const* peers, int32_t k, int64_t n, float* w, float* out,
-                               float lr, p2p_stream_t stream, int32_t recip);
+                               float lr, p2p_stream_t stream, int32_t recip, int32_t hints);
 
 static bool is_fedavg(int32_t rule) { return rule == P2P_RULE_FEDAVG || rule == P2P_RULE_FEDAVG_TORCH_GPU; }
 
@@ -53,19 +53,25 @@ extern "C" int32_t p2p_trimmed_mean_f32(const float* const* peers, int32_t k, in
                              stream);
 }
 
-extern "C" int32_t p2p_aggregate_f32(const float* const* peers, int32_t k, int64_t n, int32_t rule,
-                                     int32_t trim_b, float lr, float* w, float* out,
-                                     p2p_stream_t stream) {
-  if (!peers || (!w && !out) || k < 1 || n < 0) return P2P_ERR_INVALID;
+extern "C" int32_t p2p_aggregate_ex_f32(const float* const* peers, int32_t k, int64_t n, int32_t rule,
+                                        int32_t trim_b, float lr, float* w, float* out, int32_t hints,
+                                        p2p_stream_t stream) {
+  if (!peers || (!w && !out) || k < 1 || n < 0 || (hints & ~P2P_HINT_SHARE_CUS)) return P2P_ERR_INVALID;
   if (misaligned4(w) || misaligned4(out)) return P2P_ERR_ALIGN;
   if (is_fedavg(rule)) {
     if (n == 0) return P2P_OK;
-    return p2p_fedavg_flat_launch(peers, k, n, w, out, lr, stream, rule == P2P_RULE_FEDAVG_TORCH_GPU);
+    return p2p_fedavg_flat_launch(peers, k, n, w, out, lr, stream, rule == P2P_RULE_FEDAVG_TORCH_GPU, hints);
   }
   if (rule != P2P_RULE_MEDIAN && rule != P2P_RULE_TRIMMED) return P2P_ERR_INVALID;
   if (rule == P2P_RULE_TRIMMED && (trim_b < 0 || k - 2 * trim_b <= 0)) return P2P_ERR_INVALID;
   if (n == 0) return k > 256 ? P2P_ERR_UNSUPPORTED : P2P_OK;
   return p2p_robust_dispatch(peers, nullptr, 0, 0, k, rule, trim_b, n, w, out, lr, stream);
+}
+
+extern "C" int32_t p2p_aggregate_f32(const float* const* peers, int32_t k, int64_t n, int32_t rule,
+                                     int32_t trim_b, float lr, float* w, float* out,
+                                     p2p_stream_t stream) {
+  return p2p_aggregate_ex_f32(peers, k, n, rule, trim_b, lr, w, out, 0, stream);
 }
 
 extern "C" int32_t p2p_aggregate_segments_f32(const p2p_segment_t* segs, int32_t nseg,

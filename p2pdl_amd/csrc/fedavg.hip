@@ -713,13 +713,18 @@ constexpr bool queue_mode() {
 static std::atomic<uint32_t> g_queue_next{0};
 // The split kernel over ntiles tiles in mode MODE: the tile queue's
 // persistent grid of min(tiles, CUs) blocks when built with it (K from the
-// kernarg, K >= kQueueMinK), else one block per tile.
+// kernarg, K >= kQueueMinK), else one block per tile.  `share`
+// (P2P_HINT_SHARE_CUS): a kernel on another stream is to run beside this one
+// -- RCCL's all-gather (36.8 KiB of LDS, 8 waves of 256 VGPRs) fits no CU
+// that holds a 128-KiB split block -- so one block per tile: every tile's end
+// frees a CU the dispatcher can hand to it, where the persistent grid holds
+// every CU until the launch ends.
 template <int MODE>
 static void launch_split(const float* const* peers, int K, const int32_t* k_dev, int64_t ntiles, float* w,
                          float* out, float lr, const p2p_split_tile_t* tiles, const Seg* segs,
-                         const p2p_row_chunk_t* chunks, bool recip, hipStream_t st) {
+                         const p2p_row_chunk_t* chunks, bool recip, hipStream_t st, bool share = false) {
   const dim3 block(64 * (kSL + kSC));
-  if (queue_mode<MODE>() && !k_dev && K >= kQueueMinK) {
+  if (queue_mode<MODE>() && !share && !k_dev && K >= kQueueMinK) {
     const int q = static_cast<int>(g_queue_next.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
     const dim3 grid(static_cast<unsigned>(ntiles < device_cus() ? ntiles : device_cus()));
     if (recip)
@@ -740,12 +745,12 @@ static void launch_split(const float* const* peers, int K, const int32_t* k_dev,
 }
 
 static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, int64_t n, float* w, float* out,
-                        float lr, hipStream_t stream, bool recip = false) {
+                        float lr, hipStream_t stream, bool recip = false, bool share = false) {
   int64_t done = 0;
   {
     const int64_t tiles = split_tiles_for(K, n / kSTile);
     if (tiles > 0) {
-      launch_split<kFlat>(peers, K, k_dev, tiles, w, out, lr, nullptr, nullptr, nullptr, recip, stream);
+      launch_split<kFlat>(peers, K, k_dev, tiles, w, out, lr, nullptr, nullptr, nullptr, recip, stream, share);
       done = tiles * kSTile;
       if (done == n) return;
     }
@@ -832,8 +837,10 @@ extern "C" int32_t p2p_fedavg_split_chunks_f32(const p2p_split_tile_t* chunks, i
 }
 
 P2P_INTERNAL int32_t p2p_fedavg_flat_launch(const float* const* peers, int32_t k, int64_t n, float* w,
-                                            float* out, float lr, p2p_stream_t stream, int32_t recip) {
-  launch_flat(peers, k, nullptr, n, w, out, lr, static_cast<hipStream_t>(stream), recip != 0);
+                                            float* out, float lr, p2p_stream_t stream, int32_t recip,
+                                            int32_t hints) {
+  launch_flat(peers, k, nullptr, n, w, out, lr, static_cast<hipStream_t>(stream), recip != 0,
+              (hints & P2P_HINT_SHARE_CUS) != 0);
   return launch_status();
 }
 

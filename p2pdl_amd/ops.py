@@ -96,10 +96,14 @@ def _peer_inputs(peers: Sequence[torch.Tensor], n: int, device):
 # ------------------------------------------------------------------ K1 / K2
 def aggregate(peers: Sequence[torch.Tensor], rule="fedavg", *, w: torch.Tensor | None = None,
               out: torch.Tensor | None = None, lr: float = 0.1, trim_b: int | None = None,
-              trim_frac: float = DEFAULT_TRIM_FRAC, table: torch.Tensor | None = None) -> None:
+              trim_frac: float = DEFAULT_TRIM_FRAC, table: torch.Tensor | None = None,
+              share_cus: bool = False) -> None:
     """One flat buffer: out = rule(peers); w += lr * out (when w is given).
 
-    ``table`` may pass a prebuilt device pointer table (benchmarks reuse it)."""
+    ``table`` may pass a prebuilt device pointer table (benchmarks reuse it).
+    ``share_cus``: a kernel on another stream runs beside this call (a
+    sharded round's all-gather): P2P_HINT_SHARE_CUS, the FedAvg split
+    kernel's blocks then free CUs tile by tile (include/p2pdl.h)."""
     ref = w if w is not None else out
     if ref is None:
         raise ValueError("need w and/or out")
@@ -124,10 +128,11 @@ def aggregate(peers: Sequence[torch.Tensor], rule="fedavg", *, w: torch.Tensor |
     if n == 0:  # nothing to reduce (the reference's loops over empty tensors); an empty
         return  # tensor's data pointer is NULL, which the C ABI would refuse
     with torch.cuda.device(ref.device):
-        N.check(N.lib().p2p_aggregate_f32(table.data_ptr(), k, n, r, b, lr,
-                                          w.data_ptr() if w is not None else None,
-                                          out.data_ptr() if out is not None else None,
-                                          N.stream_handle()), "p2p_aggregate_f32")
+        N.check(N.lib().p2p_aggregate_ex_f32(table.data_ptr(), k, n, r, b, lr,
+                                             w.data_ptr() if w is not None else None,
+                                             out.data_ptr() if out is not None else None,
+                                             N.P2P_HINT_SHARE_CUS if share_cus else 0,
+                                             N.stream_handle()), "p2p_aggregate_ex_f32")
 
 
 DTYPES_16 = {torch.float16: N.P2P_DTYPE_F16, torch.bfloat16: N.P2P_DTYPE_BF16}

@@ -128,10 +128,10 @@ class PeerPlanes:
         return st + i
 
     def reduce_(self, s: int, w: torch.Tensor, rule="fedavg", *, lr: float = 0.1,
-                trim_frac: float = 0.2) -> None:
+                trim_frac: float = 0.2, share_cus: bool = False) -> None:
         from . import ops
 
-        ops.aggregate(None, rule, w=w, lr=lr, trim_frac=trim_frac, table=self.tables[s])
+        ops.aggregate(None, rule, w=w, lr=lr, trim_frac=trim_frac, table=self.tables[s], share_cus=share_cus)
 
     def aggregate_gather_(self, ws: Sequence[torch.Tensor], w_full: torch.Tensor | None = None, *,
                           rule="fedavg", lr: float = 0.1, trim_frac: float = 0.2, group=None,
@@ -161,7 +161,9 @@ class PeerPlanes:
             if hook:
                 hook(s, "reduce0", comp)
             if reduce is None:
-                self.reduce_(s, ws[s], rule, lr=lr, trim_frac=trim_frac)
+                # with an all-gather running beside it on `comm`, the reduction
+                # leaves its CUs to it tile by tile (P2P_HINT_SHARE_CUS)
+                self.reduce_(s, ws[s], rule, lr=lr, trim_frac=trim_frac, share_cus=gather and comm is not None)
             else:
                 reduce(self, s, ws[s], rule, lr, trim_frac)
             if hook:
@@ -237,10 +239,10 @@ class ChunkPlan:
         raise IndexError(i)
 
 
-def _default_reduce(peers, w, rule, lr, trim_frac):
+def _default_reduce(peers, w, rule, lr, trim_frac, share_cus=False):
     from . import ops
 
-    ops.aggregate(peers, rule, w=w, lr=lr, trim_frac=trim_frac)
+    ops.aggregate(peers, rule, w=w, lr=lr, trim_frac=trim_frac, share_cus=share_cus)
 
 
 def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor], *, rule="fedavg",
@@ -258,6 +260,7 @@ def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor],
     rank = dist.get_rank(group) if gather else 0
     n = w_full.numel()
     plan = ChunkPlan(n, world, max(1, min(chunk, -(-n // world))))
+    hip = reduce is None
     reduce = reduce or _default_reduce
     w = w_full.view(-1)
     flat_peers = [p.reshape(-1) for p in peers_full]
@@ -265,9 +268,12 @@ def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor],
     comp = torch.cuda.current_stream(w.device) if on_gpu else None
     comm = torch.cuda.Stream(w.device) if (on_gpu and overlap and gather) else None
     C, G = plan.chunk, world
+    # the HIP reduce, with all-gathers running beside it on `comm`, leaves its
+    # CUs to them tile by tile (P2P_HINT_SHARE_CUS)
+    extra = {"share_cus": True} if hip and comm is not None else {}
     for s in range(plan.full_rounds):
         st = (s * G + rank) * C
-        reduce([p[st:st + C] for p in flat_peers], w[st:st + C], rule, lr, trim_frac)
+        reduce([p[st:st + C] for p in flat_peers], w[st:st + C], rule, lr, trim_frac, **extra)
         if not gather:
             continue
         out = w[s * G * C:(s + 1) * G * C]

@@ -49,3 +49,8 @@ def test_abi_version_and_argument_errors_without_gpu():
     assert L.p2p_median_f32(1, 300, 10, 16, None) == -2  # k > 256 unsupported
     assert L.p2p_trimmed_mean_f32(1, 4, 10, 2, 16, None) == -1  # K - 2b == 0
     assert L.p2p_apply_f32(2, 16, 0.1, 10, None) == -3  # misaligned w
+    # ABI 9: launch hints; unknown bits are refused before any HIP call
+    assert L.p2p_aggregate_ex_f32(1, 3, 0, 0, 0, 0.1, 16, None, 2, None) == -1
+    assert L.p2p_aggregate_ex_f32(1, 3, 0, 0, 0, 0.1, 16, None, N.P2P_HINT_SHARE_CUS, None) == 0  # n = 0: nothing
+    assert L.p2p_fedavg_split_chunks_f32(None, 1, 16, 16, 0, 0.1, None) == -1
+    assert L.p2p_fedavg_split_chunks_f32(16, 1, 16, 16, 1, 0.1, None) == -1  # robust rule: not on the split kernel

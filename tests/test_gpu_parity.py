@@ -237,6 +237,24 @@ def test_split_kernel_repeated_launches_on_two_streams(cuda):
         assert_bits_equal(host(o), want, what=f"launch {i}")
 
 
+def test_split_kernel_share_cus_hint_same_bits(cuda):
+    """P2P_HINT_SHARE_CUS (a sharded round's all-gather beside the launch):
+    one block per tile instead of the tile queue's persistent grid -- the
+    same bits, both FedAvg rules, w and the mean."""
+    k, n, seed = 16, 2 * 256 * SPLIT_TILE + 4099, 0x5B1B
+    rows, w0 = split_case(cuda, k, n, seed, pitch_pad=64)
+    for rule in ("fedavg", "fedavg_torch_gpu"):
+        got = []
+        for share in (False, True):
+            w, out = w0.clone(), torch.empty(n, dtype=torch.float32, device=cuda)
+            ops.aggregate(rows, rule, w=w, out=out, share_cus=share)
+            got.append((host(w), host(out)))
+        assert_bits_equal(got[0][0], got[1][0], what=f"{rule} w")
+        assert_bits_equal(got[0][1], got[1][1], what=f"{rule} mean")
+        w_ref, out_ref = split_expect(k, seed, 0, 9000, torch_gpu=rule == "fedavg_torch_gpu")
+        assert_bits_equal(got[1][0][:9000], w_ref, what=f"{rule} w vs oracle")
+
+
 def test_fedavg_split_kernel_unaligned_rows_and_mean_only(cuda):
     """Rows 4-B but not 16-B aligned: the split kernel's element-wise path,
     same bits; then the mean alone (no w) through the DMA path."""
