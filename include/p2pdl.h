@@ -90,11 +90,13 @@ int64_t p2p_tile_elems(int32_t rule, int32_t k);
  *   acc = +0 (:15); acc += peers[j] for j in list order (:25-28);
  *   acc /= K (:31-32); w += fp32(lr) * acc (:36-38, lr = 0.1 there).
  * Kernel choice (a pure function of k and n, same bits either way): for
- * k >= 16, whole rounds of 8192-float tiles (a multiple of the CU count) run
- * on the LDS-DMA split kernel (loader + consumer waves; a persistent grid of
- * one block per CU claiming tiles from a counter pair of a device-global
- * ring, which each launch leaves zeroed -- see p2p_aggregate_ex_f32 for the
- * one-block-per-tile form), the rest on the VGPR kernel.  The peer pointers
+ * k >= 16, every whole 8192-float tile (from one round of the CU count up)
+ * runs on the LDS-DMA split kernel (loader + consumer waves; a persistent
+ * grid of one block per CU claiming tiles from a counter pair of a
+ * device-global ring, which each launch leaves zeroed), the < 8192-float
+ * tail on the VGPR kernel; under P2P_HINT_SHARE_CUS (p2p_aggregate_ex_f32)
+ * and on the device-K path the split kernel runs one block per tile over
+ * whole rounds of tiles and the VGPR kernel the rest.  The peer pointers
  * are read from device memory each launch; 4-byte-aligned (not 16-byte)
  * pointers are handled, more slowly. */
 int32_t p2p_fedavg_apply_f32(const float *const *peers, int32_t k, int64_t n, float *w, float lr,

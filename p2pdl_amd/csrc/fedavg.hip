@@ -677,10 +677,16 @@ static int device_cus() {
 // 8 split rounds would leave half the CUs idle in the last one.  K is the
 // kernarg or, for the device-K path, k_max.
 // Split tiles for `full` whole tiles: whole rounds of the CU count (0 below
-// one round or for K < kSplitMinK).
-static int64_t split_tiles_for(int K, int64_t full) {
+// one round or for K < kSplitMinK) -- or, for the tile queue (`all`), every
+// whole tile from one round up: its persistent blocks balance any tile count
+// dynamically, and the VGPR remainder of a partial round cost more than the
+// split kernel's own last claims (same box, alternating processes,
+// profiles/r06/alltiles: cfg3 planes +1.3-2.9%, the full job +1.0-4.0%, 64 x
+// 100M +0.2%, 16 x 100M -0.5%).
+static int64_t split_tiles_for(int K, int64_t full, bool all = false) {
   if (K < kSplitMinK || full <= 0) return 0;
   const int64_t cus = device_cus();
+  if (all) return full >= cus ? full : 0;
   return full / cus * cus;
 }
 // One block per tile: one block is resident per CU (128 KiB of LDS), so the
@@ -710,6 +716,12 @@ template <int MODE>
 constexpr bool queue_mode() {
   return P2P_SPLIT_QUEUE && MODE != kRows;
 }
+// Does a launch take the queue: its mode, no share hint, K from the kernarg
+// and long enough for the queue's publication schedule.
+template <int MODE>
+static bool use_queue(bool share, const int32_t* k_dev, int K) {
+  return queue_mode<MODE>() && !share && !k_dev && K >= kQueueMinK;
+}
 static std::atomic<uint32_t> g_queue_next{0};
 // The split kernel over ntiles tiles in mode MODE: the tile queue's
 // persistent grid of min(tiles, CUs) blocks when built with it (K from the
@@ -724,7 +736,7 @@ static void launch_split(const float* const* peers, int K, const int32_t* k_dev,
                          float* out, float lr, const p2p_split_tile_t* tiles, const Seg* segs,
                          const p2p_row_chunk_t* chunks, bool recip, hipStream_t st, bool share = false) {
   const dim3 block(64 * (kSL + kSC));
-  if (queue_mode<MODE>() && !share && !k_dev && K >= kQueueMinK) {
+  if (use_queue<MODE>(share, k_dev, K)) {
     const int q = static_cast<int>(g_queue_next.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
     const dim3 grid(static_cast<unsigned>(ntiles < device_cus() ? ntiles : device_cus()));
     if (recip)
@@ -748,7 +760,7 @@ static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, 
                         float lr, hipStream_t stream, bool recip = false, bool share = false) {
   int64_t done = 0;
   {
-    const int64_t tiles = split_tiles_for(K, n / kSTile);
+    const int64_t tiles = split_tiles_for(K, n / kSTile, use_queue<kFlat>(share, k_dev, K));
     if (tiles > 0) {
       launch_split<kFlat>(peers, K, k_dev, tiles, w, out, lr, nullptr, nullptr, nullptr, recip, stream, share);
       done = tiles * kSTile;
