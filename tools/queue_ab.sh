@@ -12,7 +12,10 @@ B="bench.py --no-sub --no-cpu-baseline --no-reference-gpu --steps 10 --warmup 2"
 for i in $(seq 1 "$R"); do
   for spec in "$@"; do
     name=${spec%%|*}; args=${spec#*|}
-    for lib in ${OTHER:-noqueue} prod; do
+    # ABBA: the first process of a pair read 2-3% faster on these boxes,
+    # whichever build it was (profiles/r06/queue_ab/README.md)
+    if [ $((i % 2)) = 1 ]; then order="${OTHER:-noqueue} prod"; else order="prod ${OTHER:-noqueue}"; fi
+    for lib in $order; do
       if [ $lib = prod ]; then L=""; else L="P2P_LIB=tools/libp2pdl_$lib.so"; fi
       env $L timeout -k 10 240 python3 -u $B $args > "$OUT/${lib}_${name}_$i.json" 2> "$OUT/${lib}_${name}_$i.err" \
         || { tail "$OUT/${lib}_${name}_$i.err"; exit 1; }
