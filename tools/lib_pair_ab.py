@@ -7,9 +7,11 @@ boxes: whichever build ran first in a round read 2-3% faster, whatever it was
 process (ctypes, the same ABI), the same device buffers are reduced by each
 in turn, rep by rep, each launch queued behind a spin kernel and timed with
 HIP events; the builds' outputs are bit-compared.  Flat FedAvg
-(p2p_aggregate_f32), one launch per case -- the cfg3 plane shapes and others.
+(p2p_aggregate_f32), one launch per case -- the cfg3 plane shapes and others
+-- and ("sd:K:scale") a state_dict of separately allocated tensors on the
+chunk list (p2p_fedavg_split_chunks_f32, tables built once by the product).
 Measurement tool, not product.
-usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n> ...
+usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n | sd:K:scale> ...
   tag "prod" = p2pdl_amd/libp2pdl_hip.so, tag X = tools/libp2pdl_X.so"""
 import ctypes
 import os
@@ -31,18 +33,85 @@ def load(tag):
     f.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     f.restype = ctypes.c_int32
-    return f
+    c = lib.p2p_fedavg_split_chunks_f32
+    c.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+                  ctypes.c_void_p]
+    c.restype = ctypes.c_int32
+    return f, c
+
+
+def state_dict_case(fns, tags, K, scale, reps, dev):
+    """ResNet-18's 62 shapes x scale as separately allocated tensors x K: the
+    chunk list and segment table built once by the product's host code
+    (ops.aggregate_ptr_table_, the model tensors `ws` it points at kept),
+    then every build's chunk kernel over the same tables."""
+    import bench
+
+    sizes = [int(np.prod(sh)) for _, sh in bench.resnet18_param_shapes()] * scale
+    peers = [[torch.empty(m, dtype=torch.float32, device=dev) for m in sizes] for _ in range(K)]
+    for p in range(K):
+        for l, t in enumerate(peers[p]):
+            ops.fill_synthetic_(t, 0x5EED0001 + l, p, 1e-2)
+    w0 = [torch.empty(m, dtype=torch.float32, device=dev) for m in sizes]
+    for l, w in enumerate(w0):
+        ops.fill_synthetic_(w, 0x5EED0001 + l, 0xFFFFF, 5e-2)
+    ptrs = np.array([[peers[p][l].data_ptr() for p in range(K)] for l in range(len(sizes))], dtype=np.uint64)
+    ws = [w.clone() for w in w0]
+    ops._TABLES.clear()
+    ops.aggregate_ptr_table_(ws, ptrs, "fedavg")
+    entry = next(reversed(ops._TABLES.values()))
+    lst_off, S, segs_off, how = entry[5][2]
+    assert how == "chunks" and entry[1] == 0, "every key on the chunk list"
+    base = entry[0].data_ptr()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    outs = {}
+    for t in tags:
+        for w, a in zip(ws, w0):
+            w.copy_(a)
+        assert fns[t][1](base + lst_off, S, base + segs_off, K, 0, 0.1, st) == 0
+        torch.cuda.synchronize()
+        outs[t] = torch.cat(ws).cpu().numpy().view(np.uint32)
+    same = all(np.array_equal(outs[t], outs[tags[0]]) for t in tags)
+    ms = {t: [] for t in tags}
+    for r in range(reps):
+        for t in (tags if r % 2 == 0 else tags[::-1]):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(2_000_000)
+            e0.record()
+            fns[t][1](base + lst_off, S, base + segs_off, K, 0, 0.1, st)
+            e1.record()
+            torch.cuda.synchronize()
+            ms[t].append(e0.elapsed_time(e1))
+    report(f"state_dict K={K} x{scale} ({len(sizes)} separately allocated tensors, chunk list)", K, sum(sizes), same, ms)
+    del peers, ws, w0
+    ops._TABLES.clear()
+    torch.cuda.empty_cache()
+    return same
+
+
+def report(title, K, n, same, ms):
+    alg = 4.0 * n * (K + 2)
+    print(f"{title} n={n:,}  bit-identical across builds: {same}")
+    for t, v in ms.items():
+        v = sorted(v)
+        med = v[len(v) // 2]
+        print(f"  {t:10s} median {med:.4f} ms  {alg / med / 1e6 / 8000:.4f} of 8 TB/s  best {alg / v[0] / 1e6 / 8000:.4f}"
+              f"  worst {alg / v[-1] / 1e6 / 8000:.4f}", flush=True)
 
 
 def main():
     i = sys.argv.index("--")
     reps, tags = int(sys.argv[1]), sys.argv[2:i]
-    cases = [tuple(int(x) for x in c.split(":")) for c in sys.argv[i + 1:]]
+    cases = [c.split(":") for c in sys.argv[i + 1:]]  # "K:n" flat, "sd:K:scale" a chunk-list state_dict
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     fns = {t: load(t) for t in tags}
     ok = True
-    for K, n in cases:
+    for case in cases:
+        if case[0] == "sd":
+            ok &= state_dict_case(fns, tags, int(case[1]), int(case[2]), reps, dev)
+            continue
+        K, n = int(case[0]), int(case[1])
         pitch = -(-n // 64) * 64
         slab = torch.empty((K, pitch), dtype=torch.float32, device=dev)
         for p in range(K):
@@ -54,7 +123,7 @@ def main():
         st = torch.cuda.current_stream(dev).cuda_stream
         for t, f in fns.items():
             w = w0.clone()
-            assert f(table.data_ptr(), K, n, 0, 0, 0.1, w.data_ptr(), None, st) == 0
+            assert f[0](table.data_ptr(), K, n, 0, 0, 0.1, w.data_ptr(), None, st) == 0
             torch.cuda.synchronize()
             outs[t] = w.cpu().numpy().view(np.uint32)
         same = all(np.array_equal(outs[t], outs[tags[0]]) for t in tags)
@@ -67,17 +136,11 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 torch.cuda._sleep(2_000_000)
                 e0.record()
-                fns[t](table.data_ptr(), K, n, 0, 0, 0.1, w.data_ptr(), None, st)
+                fns[t][0](table.data_ptr(), K, n, 0, 0, 0.1, w.data_ptr(), None, st)
                 e1.record()
                 torch.cuda.synchronize()
                 ms[t].append(e0.elapsed_time(e1))
-        alg = 4.0 * n * (K + 2)
-        print(f"K={K} n={n:,}  bit-identical across builds: {same}")
-        for t, v in ms.items():
-            v = sorted(v)
-            med = v[len(v) // 2]
-            print(f"  {t:10s} median {med:.4f} ms  {alg / med / 1e6 / 8000:.4f} of 8 TB/s  best {alg / v[0] / 1e6 / 8000:.4f}"
-                  f"  worst {alg / v[-1] / 1e6 / 8000:.4f}", flush=True)
+        report(f"flat K={K}", K, n, same, ms)
         del slab, table, w0, w
         torch.cuda.empty_cache()
     return 0 if ok else 1
