@@ -511,6 +511,7 @@ enum SplitMode { kFlat = 0, kSegs = 1, kRows = 2, kChunks = 3 };
 // finish zeroes the counter for the stream's next launch.
 constexpr int kQW = 2, kQR = 4;
 constexpr int kQueueMinK = kQR + kSS;  // K the queue's publication schedule needs
+constexpr int kQueueMaxK = 128;        // above it one block per tile (see queue_mode)
 constexpr int kQueueSlots = 4096;      // counter pairs, one per launch in flight (see launch_split)
 __device__ int32_t g_tile_queue[2 * kQueueSlots];
 
@@ -680,9 +681,8 @@ static int device_cus() {
 // one round or for K < kSplitMinK) -- or, for the tile queue (`all`), every
 // whole tile from one round up: its persistent blocks balance any tile count
 // dynamically, and the VGPR remainder of a partial round cost more than the
-// split kernel's own last claims (same box, alternating processes,
-// profiles/r06/alltiles: cfg3 planes +1.3-2.9%, the full job +1.0-4.0%, 64 x
-// 100M +0.2%, 16 x 100M -0.5%).
+// split kernel's own last claims (same process, profiles/r06/pair_ab: 64 /
+// 16 x 11.7M +3.0% / +5.7%, 64 / 16 x 100M +0.2% / +0.3%).
 static int64_t split_tiles_for(int K, int64_t full, bool all = false) {
   if (K < kSplitMinK || full <= 0) return 0;
   const int64_t cus = device_cus();
@@ -704,11 +704,16 @@ static dim3 split_grid(int64_t tiles) { return dim3(static_cast<unsigned>(tiles)
 // launch keeps its pair: its replays on one stream run in order).  A pair is
 // reused kQueueSlots launches later: the bound is that many split launches
 // in flight at once on one device.
-// Which launches take the queue (same-box A/Bs, alternating processes,
-// profiles/r06/queue_ab): flat buffers -- the cfg3 planes +2.8-5.1%, the
-// full job +0.4-2.7%, 16 x 100M +5.7% -- and segment / chunk lists (the
-// drop-in's general path, within +-0.5%); not the rows kernel (cfg2 landed
-// -0.4 to -1.0%).  An A/B build may set P2P_SPLIT_QUEUE 0 (no queue at all).
+// Which launches take the queue: K <= kQueueMaxK, not the rows kernel.  Same
+// process, the builds alternated launch by launch on the same buffers
+// (tools/lib_pair_ab.py, profiles/r06/pair_ab): flat buffers at K = 16 / 64
+// +5.9-7.0% / +1.5-2.5%, chunk-list state_dicts +1.1-2.3% -- but the K = 256
+// cfg3 planes -1.0 to -2.2%, where a tile's epilogue is 1/256 of its time
+// and the queue's claims cost more than they hide.  (Process-level A/Bs had
+// credited the queue with +3% at K = 256: the first process of a pair ran
+// faster whichever build it was, profiles/r06/queue_ab/README.md.)  The rows
+// kernel (cfg2 landed) lost 0.4-1.0% even at K = 64.  An A/B build may set
+// P2P_SPLIT_QUEUE 0 (no queue at all).
 #ifndef P2P_SPLIT_QUEUE
 #define P2P_SPLIT_QUEUE 1
 #endif
@@ -716,11 +721,11 @@ template <int MODE>
 constexpr bool queue_mode() {
   return P2P_SPLIT_QUEUE && MODE != kRows;
 }
-// Does a launch take the queue: its mode, no share hint, K from the kernarg
-// and long enough for the queue's publication schedule.
+// Does a launch take the queue: its mode, no share hint, K from the kernarg,
+// long enough for the queue's publication schedule and at most kQueueMaxK.
 template <int MODE>
 static bool use_queue(bool share, const int32_t* k_dev, int K) {
-  return queue_mode<MODE>() && !share && !k_dev && K >= kQueueMinK;
+  return queue_mode<MODE>() && !share && !k_dev && K >= kQueueMinK && K <= kQueueMaxK;
 }
 static std::atomic<uint32_t> g_queue_next{0};
 // The split kernel over ntiles tiles in mode MODE: the tile queue's
