@@ -11,7 +11,9 @@ HIP events; the builds' outputs are bit-compared.  Flat FedAvg
 -- and ("sd:K:scale") a state_dict of separately allocated tensors on the
 chunk list (p2p_fedavg_split_chunks_f32, tables built once by the product).
 Measurement tool, not product.
-usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n | sd:K:scale> ...
+and ("rows:K:scale") the same model landed in a DeviceInbox slab (the rows
+kernel).
+usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n | sd:K:scale | rows:K:scale> ...
   tag "prod" = p2pdl_amd/libp2pdl_hip.so, tag X = tools/libp2pdl_X.so"""
 import ctypes
 import os
@@ -37,7 +39,58 @@ def load(tag):
     c.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
                   ctypes.c_void_p]
     c.restype = ctypes.c_int32
-    return f, c
+    r = lib.p2p_fedavg_split_rows_f32
+    r.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_float,
+                  ctypes.c_void_p]
+    r.restype = ctypes.c_int32
+    return f, c, r
+
+
+def rows_case(fns, tags, K, scale, reps, dev):
+    """ResNet-18's shapes x scale landed in a DeviceInbox slab x K: the rows
+    kernel's row table and chunk table built once by the product's host code
+    (ops.aggregate_slab_rows_), then every build's rows kernel over them."""
+    import bench
+    from p2pdl_amd.node.inbox import DeviceInbox
+
+    sizes = [int(np.prod(sh)) for _, sh in bench.resnet18_param_shapes()] * scale
+    w0 = [torch.empty(m, dtype=torch.float32, device=dev) for m in sizes]
+    for l, w in enumerate(w0):
+        ops.fill_synthetic_(w, 0x5EED0001 + l, 0xFFFFF, 5e-2)
+    inbox = DeviceInbox({f"k{l}": w for l, w in enumerate(w0)}, k_max=K, device=dev)
+    for p in range(K):
+        ops.fill_synthetic_(inbox.slab[p], 0x5EED0001, p, 1e-2)
+    offs = [inbox.layout[f"k{l}"][0] for l in range(len(sizes))]
+    ws = [w.clone() for w in w0]
+    ops._TABLES.clear()
+    entry = ops.aggregate_slab_rows_(ws, inbox.slab, list(range(K)), offs, "fedavg")
+    assert entry[5][0] == "rows"
+    _, ch_off, ntiles = entry[5]
+    base = entry[0].data_ptr()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    outs = {}
+    for t in tags:
+        for w, a in zip(ws, w0):
+            w.copy_(a)
+        assert fns[t][2](base, K, ntiles, base + ch_off, 0, 0.1, st) == 0
+        torch.cuda.synchronize()
+        outs[t] = torch.cat(ws).cpu().numpy().view(np.uint32)
+    same = all(np.array_equal(outs[t], outs[tags[0]]) for t in tags)
+    ms = {t: [] for t in tags}
+    for r in range(reps):
+        for t in (tags if r % 2 == 0 else tags[::-1]):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(2_000_000)
+            e0.record()
+            fns[t][2](base, K, ntiles, base + ch_off, 0, 0.1, st)
+            e1.record()
+            torch.cuda.synchronize()
+            ms[t].append(e0.elapsed_time(e1))
+    report(f"rows K={K} x{scale} (DeviceInbox slab rows, {ntiles} tiles)", K, sum(sizes), same, ms)
+    del inbox, ws, w0
+    ops._TABLES.clear()
+    torch.cuda.empty_cache()
+    return same
 
 
 def state_dict_case(fns, tags, K, scale, reps, dev):
@@ -108,8 +161,9 @@ def main():
     fns = {t: load(t) for t in tags}
     ok = True
     for case in cases:
-        if case[0] == "sd":
-            ok &= state_dict_case(fns, tags, int(case[1]), int(case[2]), reps, dev)
+        if case[0] in ("sd", "rows"):
+            fn = state_dict_case if case[0] == "sd" else rows_case
+            ok &= fn(fns, tags, int(case[1]), int(case[2]), reps, dev)
             continue
         K, n = int(case[0]), int(case[1])
         pitch = -(-n // 64) * 64
