@@ -704,22 +704,23 @@ static dim3 split_grid(int64_t tiles) { return dim3(static_cast<unsigned>(tiles)
 // launch keeps its pair: its replays on one stream run in order).  A pair is
 // reused kQueueSlots launches later: the bound is that many split launches
 // in flight at once on one device.
-// Which launches take the queue: K <= kQueueMaxK, not the rows kernel.  Same
+// Which launches take the queue: K <= kQueueMaxK, every mode.  Same
 // process, the builds alternated launch by launch on the same buffers
 // (tools/lib_pair_ab.py, profiles/r06/pair_ab): flat buffers at K = 16 / 64
-// +5.9-7.0% / +1.5-2.5%, chunk-list state_dicts +1.1-2.3% -- but the K = 256
-// cfg3 planes -1.0 to -2.2%, where a tile's epilogue is 1/256 of its time
-// and the queue's claims cost more than they hide.  (Process-level A/Bs had
-// credited the queue with +3% at K = 256: the first process of a pair ran
-// faster whichever build it was, profiles/r06/queue_ab/README.md.)  The rows
-// kernel (cfg2 landed) lost 0.4-1.0% even at K = 64.  An A/B build may set
-// P2P_SPLIT_QUEUE 0 (no queue at all).
+// +5.9-7.0% / +1.5-2.5%, chunk-list state_dicts +1.1-2.3%, the rows kernel
+// (cfg2 landed) +1.4-2.4% -- but the K = 256 cfg3 planes -2.2 to +0.5%
+// (the short plane -2%), where a tile's epilogue is 1/256 of its time and
+// the queue's claims cost about what they hide.  (Process-level A/Bs had
+// credited the queue with +3% at K = 256 and debited the rows kernel 1%:
+// the first process of a pair ran faster whichever build it was,
+// profiles/r06/queue_ab/README.md.)  An A/B build may set P2P_SPLIT_QUEUE 0
+// (no queue at all).
 #ifndef P2P_SPLIT_QUEUE
 #define P2P_SPLIT_QUEUE 1
 #endif
 template <int MODE>
 constexpr bool queue_mode() {
-  return P2P_SPLIT_QUEUE && MODE != kRows;
+  return P2P_SPLIT_QUEUE && MODE >= kFlat;
 }
 // Does a launch take the queue: its mode, no share hint, K from the kernarg,
 // long enough for the queue's publication schedule and at most kQueueMaxK.
