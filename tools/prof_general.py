@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Host profile (round 6) of the drop-in's general path with a NEW device
+table every call -- a round whose pickle.loads updates arrive at new
+addresses: aggregate_models over plain dicts of separately allocated
+tensors (ResNet-18 x 64), ops._TABLES cleared before each call, cProfile
+over the calls.  Measurement tool, not product.
+usage: python tools/prof_general.py [calls]"""
+import cProfile
+import io
+import os
+import pstats
+import sys
+import time
+import types
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from p2pdl_amd import ops  # noqa: E402
+from p2pdl_amd.aggregator import aggregation as agg  # noqa: E402
+
+
+def main():
+    calls = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+    dev = torch.device("cuda", 0)
+    K = 64
+    shapes = bench.resnet18_param_shapes()
+    model = torch.nn.Module()
+    for nm, sh in shapes:
+        model.register_parameter(nm.replace(".", "__"), torch.nn.Parameter(
+            torch.zeros(sh, dtype=torch.float32, device=dev), requires_grad=False))
+    keys = [nm.replace(".", "__") for nm, _ in shapes]
+    upd = [{k: torch.full(sh, 1e-3 * j, dtype=torch.float32, device=dev) for k, (_, sh) in zip(keys, shapes)}
+           for j in range(K)]
+    agg.broadcast_global_model_update = lambda self: None
+    node = types.SimpleNamespace(model=model, trainers_list=[0] * K, addr="127.0.0.1", port=1, neighbors=[],
+                                 received_models=[])
+
+    def call():
+        node.received_models.extend({"model": u, "sender": j} for j, u in enumerate(upd))
+        ops._TABLES.clear()
+        agg.aggregate_models(node)
+
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    t = []
+    for _ in range(calls):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        call()
+        torch.cuda.synchronize()
+        t.append(time.perf_counter() - t0)
+    print(f"new table every call: median {np.median(t) * 1e6:.1f} us per call (host wall, synchronised)")
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(calls):
+        call()
+    torch.cuda.synchronize()
+    pr.disable()
+    s = io.StringIO()
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
+    print(s.getvalue())
+
+
+if __name__ == "__main__":
+    main()
