@@ -478,6 +478,36 @@ def test_fedavg_chunks_through_pickle_loads(cuda, monkeypatch):
     assert launches == ["p2p_fedavg_split_chunks_f32"] * 2
 
 
+@pytest.mark.parametrize("k", [1, 3, 6, 7, 8, 16])
+def test_split_chunks_abi_any_k(cuda, k):
+    """p2p_fedavg_split_chunks_f32 called through the C ABI with K below the
+    product's K >= 16 plan -- around the tile queue's K >= 7 threshold
+    (below it one block per tile) -- over more than one round of tiles:
+    bit-exact per key against the oracle."""
+    from p2pdl_amd import _host_tables
+
+    seed, sizes = 0xC7 + k, [1_234_567, 3, 1_000_005]
+    ws, peer_lists, hp, hw = _chunk_case(cuda, k, sizes, seed)
+    L = len(sizes)
+    nch = np.array([-(-n // 1024) for n in sizes], dtype=np.int64)
+    ntiles = -(-int(nch.sum()) // 8)
+    lst = np.empty(ntiles * 8, dtype=ops._SPLIT_DTYPE)
+    assert _host_tables.fill_chunk_list(nch, lst) == int(nch.sum())
+    rows = torch.tensor([[peer_lists[p][l].data_ptr() for p in range(k)] for l in range(L)], dtype=torch.int64,
+                        device=cuda)
+    segs = np.zeros(L, dtype=ops._SEG_DTYPE)
+    segs["peers"] = [rows[l].data_ptr() for l in range(L)]
+    segs["w"] = [w.data_ptr() for w in ws]
+    segs["n"] = sizes
+    segs_d = torch.from_numpy(segs.view(np.uint8).copy()).to(cuda)
+    lst_d = torch.from_numpy(lst.view(np.uint8).copy()).to(cuda)
+    ops.N.check(ops.N.lib().p2p_fedavg_split_chunks_f32(lst_d.data_ptr(), ntiles, segs_d.data_ptr(), k, 0, 0.1,
+                                                        ops.N.stream_handle()), "split_chunks")
+    torch.cuda.synchronize()
+    for l in range(L):
+        assert_bits_equal(host(ws[l]), oracle.fedavg(hp[l], hw[l])[0], what=f"K={k} key {l}")
+
+
 def test_chunk_plan_host_logic(cuda):
     """The chunk list itself: aligned keys only, 1024-element chunks in key
     order, c0 per chunk, the last tile padded with seg -1; K < 16, robust

@@ -41,7 +41,7 @@ while IFS=: read -r w k c p extra; do
 done <<'EOS'
 cfg3:fedavg_split_kernel+fedavg_flat_kernel:15625000:256:--workload cfg3
 cfg3-chunk:fedavg_split_kernel+fedavg_flat_kernel:15625000:256:--job cfg3-full --steps 1
-cfg2-dropin:fedavg_split_kernel<false, 2, false>:11689512:64:--workload cfg2-dropin
+cfg2-dropin:fedavg_split_kernel<false, 2,:11689512:64:--workload cfg2-dropin
 cfg4-median:robust_flat_kernel:25000000:128:--workload cfg4-median
 cfg4-trimmed:robust_flat_kernel:25000000:128:--workload cfg4-trimmed
 median256:robust_median_pair_kernel:12500000:256:--workload median256
