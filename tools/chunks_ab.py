@@ -92,11 +92,25 @@ def one_case(K, scale, reps, dev):
         ops.fill_synthetic_(inbox.slab[p], 0x5EED0001, p, 1e-2)
     offs = [inbox.layout[f"k{l}"][0] for l in range(len(sizes))]
     ws = [w.clone() for w in w0]
-    ms["rows (inbox slab)"] = []
     ops.aggregate_slab_rows_(ws, inbox.slab, list(range(K)), offs, "fedavg")
-    for _ in range(reps):
-        timed(lambda: ops.aggregate_slab_rows_(ws, inbox.slab, list(range(K)), offs, "fedavg"),
-              ms["rows (inbox slab)"], dev)
+    # the chunk list over the SAME slab memory (plain views of the rows): the
+    # chunk kernel against the rows kernel with the memory layout held fixed,
+    # alternated rep by rep
+    vptrs = np.array([[inbox.slab[p, offs[l]:offs[l] + sizes[l]].data_ptr() for p in range(K)]
+                      for l in range(len(sizes))], dtype=np.uint64)
+    ws2 = [w.clone() for w in w0]
+    saved_route = ops.STATE_DICT_ROUTE
+    ms["rows (inbox slab)"], ms["chunks (slab views)"] = [], []
+    try:
+        ops.STATE_DICT_ROUTE = "chunks"
+        ops.aggregate_ptr_table_(ws2, vptrs, "fedavg")
+        for _ in range(reps):
+            timed(lambda: ops.aggregate_slab_rows_(ws, inbox.slab, list(range(K)), offs, "fedavg"),
+                  ms["rows (inbox slab)"], dev)
+            timed(lambda: ops.aggregate_ptr_table_(ws2, vptrs, "fedavg"), ms["chunks (slab views)"], dev)
+    finally:
+        ops.STATE_DICT_ROUTE = saved_route
+        ops._TABLES.clear()
     table = ops.pointer_table([inbox.slab[p, :nflat] for p in range(K)], dev)
     wf = torch.empty(nflat, dtype=torch.float32, device=dev)
     ms["flat (same bytes)"] = []
