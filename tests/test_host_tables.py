@@ -55,3 +55,16 @@ def test_sparse_cuda_tensor_defers_to_python_path(cuda):
     got = _host_tables.gather_peer_table([{"model": {"a": dense}}, {"model": {"a": sp}}], ["a"], [2],
                                          cuda.index, _table(1, 2))
     assert got == 1
+
+
+def test_fill_chunk_list():
+    """The split kernel's chunk list (include/p2pdl.h
+    p2p_fedavg_split_chunks_f32): (segment, first element) per 1024-element
+    chunk in key order, keys with no chunks skipped, the rest (-1, 0);
+    -1 (nothing claimed) when the chunks do not fit."""
+    nch = np.array([3, 0, 1, 2], dtype=np.int64)
+    out = np.full((8, 2), 7, dtype=np.int64)
+    assert _host_tables.fill_chunk_list(nch, out) == 6
+    assert out.tolist() == [[0, 0], [0, 1024], [0, 2048], [2, 0], [3, 0], [3, 1024], [-1, 0], [-1, 0]]
+    assert _host_tables.fill_chunk_list(np.array([9], dtype=np.int64), np.zeros((8, 2), dtype=np.int64)) == -1
+    assert _host_tables.fill_chunk_list(np.array([-1], dtype=np.int64), np.zeros((8, 2), dtype=np.int64)) == -1

@@ -102,3 +102,31 @@ def test_key_paths_are_integer_networks(funcs):
             assert _count(c, INT_MINMAX) > 0, name
             checked += 1
     assert checked >= 8
+
+
+def test_no_scalar_memory_writes_anywhere(funcs):
+    """No function of the library writes through the scalar data cache (no
+    scalar stores, scalar atomics or scalar-cache write-back / discard): every
+    store, and the tile queue's claim atomics, are vector memory ops."""
+    bad = {name: [op for op in c if op.startswith(("s_store", "s_buffer_store", "s_atomic", "s_buffer_atomic",
+                                                    "s_dcache_wb", "s_dcache_discard", "s_scratch_store"))]
+           for name, c in funcs.items()}
+    bad = {k: v for k, v in bad.items() if v}
+    assert not bad, bad
+
+
+def test_split_kernel_modes_and_queue_present(funcs):
+    """The split kernel's modes (flat 0, segments 1, rows 2, chunks 3) are
+    built with and without the tile queue; the queued ones claim tiles with a
+    vector atomic add; the chunk list's loaders DMA through buffer loads
+    (lanes past a key's end masked by the descriptor)."""
+    split = {n: c for n, c in funcs.items() if "fedavg_split_kernel" in n}
+    for mode in range(4):
+        for q in (0, 1):
+            assert any(f"ILb0ELi{mode}ELb{q}E" in n for n in split), (mode, q)
+    for n, c in split.items():
+        if "ELb1EE" in n:  # QUEUE
+            assert c["global_atomic_add"] + c["global_atomic_add_u32"] + sum(
+                v for k, v in c.items() if k.startswith("global_atomic_add")) >= 1, n
+        if "ELi3E" in n:  # CHUNKS
+            assert sum(v for k, v in c.items() if k.startswith("buffer_load_dwordx4")) >= 1, n
