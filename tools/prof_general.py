@@ -4,7 +4,7 @@ table every call -- a round whose pickle.loads updates arrive at new
 addresses: aggregate_models over plain dicts of separately allocated
 tensors (ResNet-18 x 64), ops._TABLES cleared before each call, cProfile
 over the calls.  Measurement tool, not product.
-usage: python tools/prof_general.py [calls]"""
+usage: python tools/prof_general.py [calls] [mlp]"""
 import cProfile
 import io
 import os
@@ -24,9 +24,10 @@ from p2pdl_amd.aggregator import aggregation as agg  # noqa: E402
 
 def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+    mlp = len(sys.argv) > 2 and sys.argv[2] == "mlp"  # cfg1: the MNIST MLP x 3
     dev = torch.device("cuda", 0)
-    K = 64
-    shapes = bench.resnet18_param_shapes()
+    K = 3 if mlp else 64
+    shapes = bench.MLP_SHAPES if mlp else bench.resnet18_param_shapes()
     model = torch.nn.Module()
     for nm, sh in shapes:
         model.register_parameter(nm.replace(".", "__"), torch.nn.Parameter(
@@ -61,7 +62,7 @@ def main():
     torch.cuda.synchronize()
     pr.disable()
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(40)
     print(s.getvalue())
 
 
