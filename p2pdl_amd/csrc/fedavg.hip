@@ -510,7 +510,14 @@ enum SplitMode { kFlat = 0, kSegs = 1, kRows = 2, kChunks = 3 };
 // stage is due ((j+1)K - kSS + 1 > jK + kQR for K >= 8).  The last block to
 // finish zeroes the counter for the stream's next launch.
 constexpr int kQW = 2, kQR = 4;
-constexpr int kQueueMinK = kQR + kSS;  // K the queue's publication schedule needs
+// P2P_QUEUE_LATE (an A/B build): claim the next tile after barrier K - 8 of
+// the current one, publish it after K - 5, the loaders read it after K - 4 --
+// a tile is reserved for ~8 stages before its block starts it, where the
+// early schedule reserves it for a whole tile (K >= 8 needed).
+#ifndef P2P_QUEUE_LATE
+#define P2P_QUEUE_LATE 0
+#endif
+constexpr int kQueueMinK = P2P_QUEUE_LATE ? 8 : kQR + kSS;  // K the queue's publication schedule needs
 constexpr int kQueueMaxK = 128;        // above it one block per tile (see queue_mode)
 constexpr int kQueueSlots = 4096;      // counter pairs, one per launch in flight (see launch_split)
 __device__ int32_t g_tile_queue[2 * kQueueSlots];
@@ -574,7 +581,7 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // stage i landed; stage i-1's slot read
       if constexpr (QUEUE) {
-        if (kb == kQR) {  // the block's next tile, published after barrier kQW of this one
+        if (kb == (P2P_QUEUE_LATE ? K - 4 : kQR)) {  // the block's next tile, published after barrier kQW of this one
           tnext = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(tq[(jb + 1) & 3])));
           if (tnext < ntiles) N += K;
         }
@@ -607,9 +614,10 @@ __global__ __launch_bounds__(64 * (kSL + kSC)) void fedavg_split_kernel(const fl
     int64_t t = b;
     for (int j = 0;; ++j) {
       int64_t claim = 0;
-      if (cw == 0 && lane == 0) claim = G + atomicAdd(&queue[0], 1);
+      if (!P2P_QUEUE_LATE && cw == 0 && lane == 0) claim = G + atomicAdd(&queue[0], 1);
       tile(t, [&](int k) {
-        if (k == kQW && cw == 0) {
+        if (P2P_QUEUE_LATE && k == K - 8 && cw == 0 && lane == 0) claim = G + atomicAdd(&queue[0], 1);
+        if (k == (P2P_QUEUE_LATE ? K - 5 : kQW) && cw == 0) {
           if (lane == 0) tq[(j + 1) & 3] = claim;
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
