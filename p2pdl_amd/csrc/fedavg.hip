@@ -503,22 +503,29 @@ enum SplitMode { kFlat = 0, kSegs = 1, kRows = 2, kChunks = 3 };
 // block per tile.  A block's loaders then stream tile j+1's first stages
 // during tile j's epilogue (w DMA wait, / K, apply, stores), which a
 // one-tile block leaves the CU idle for.  Consumer wave 0 claims the next
-// tile (a vector atomic) when it starts a tile and publishes it in LDS after
-// the tile's barrier kQW; every wave reads it after barrier kQR (loaders) or
-// after the tile (consumers), so the loaders know the next tile -- or that
-// there is none: the same barrier count on both sides -- before its first
-// stage is due ((j+1)K - kSS + 1 > jK + kQR for K >= 8).  The last block to
-// finish zeroes the counter for the stream's next launch.
+// tile (a vector atomic) late in the current tile and publishes it in LDS
+// a few barriers later; every wave reads it after a later barrier (loaders)
+// or after the tile (consumers), so the loaders know the next tile -- or
+// that there is none: the same barrier count on both sides -- before its
+// first stage is due (the schedule below).  The last block to finish zeroes
+// the counter for the stream's next launch.
 constexpr int kQW = 2, kQR = 4;
-// P2P_QUEUE_LATE (an A/B build): claim the next tile after barrier K - 8 of
-// the current one, publish it after K - 5, the loaders read it after K - 4 --
-// a tile is reserved for ~8 stages before its block starts it, where the
-// early schedule reserves it for a whole tile (K >= 8 needed).
+// The claim schedule.  LATE (the product): claim the next tile after barrier
+// K - 8 of the current one, publish it after K - 5, the loaders read it
+// after K - 4 -- a tile is reserved for ~8 stages (~10 us) before its block
+// starts it (K >= 8 needed).  Early (P2P_QUEUE_LATE 0, an A/B build): claim
+// at the tile's start, publish after barrier kQW, read after kQR -- a tile
+// reserved for a whole tile time (~300 us at K = 256), which left the last
+// tiles of a launch waiting on busy blocks while others idled.  Same
+// process, alternated launch by launch (profiles/r06/pair_ab/
+// pair_ab_box8_qlate.log): late against early at K = 256 x 16.8M +0.7%,
+// 16 x 100M +1.3%, cfg2 rows +1.7%, chunk list +1.4%.
 #ifndef P2P_QUEUE_LATE
-#define P2P_QUEUE_LATE 0
+#define P2P_QUEUE_LATE 1
 #endif
 constexpr int kQueueMinK = P2P_QUEUE_LATE ? 8 : kQR + kSS;  // K the queue's publication schedule needs
-constexpr int kQueueMaxK = 128;        // above it one block per tile (see queue_mode)
+constexpr int kQueueMaxK = 256;        // above it one block per tile (see queue_mode)
+constexpr int kAllTilesMaxK = 128;     // above it whole CU rounds even when queued (see split_tiles_for)
 constexpr int kQueueSlots = 4096;      // counter pairs, one per launch in flight (see launch_split)
 __device__ int32_t g_tile_queue[2 * kQueueSlots];
 
@@ -712,15 +719,15 @@ static dim3 split_grid(int64_t tiles) { return dim3(static_cast<unsigned>(tiles)
 // launch keeps its pair: its replays on one stream run in order).  A pair is
 // reused kQueueSlots launches later: the bound is that many split launches
 // in flight at once on one device.
-// Which launches take the queue: K <= kQueueMaxK, every mode.  Same
+// Which launches take the queue: 8 <= K <= kQueueMaxK, every mode.  Same
 // process, the builds alternated launch by launch on the same buffers
-// (tools/lib_pair_ab.py, profiles/r06/pair_ab): flat buffers at K = 16 / 64
-// +5.9-7.0% / +1.5-2.5%, chunk-list state_dicts +1.1-2.3%, the rows kernel
-// (cfg2 landed) +1.4-2.4% -- but the K = 256 cfg3 planes -2.2 to +0.5%
-// (the short plane -2%), where a tile's epilogue is 1/256 of its time and
-// the queue's claims cost about what they hide.  (Process-level A/Bs had
-// credited the queue with +3% at K = 256 and debited the rows kernel 1%:
-// the first process of a pair ran faster whichever build it was,
+// (tools/lib_pair_ab.py, profiles/r06/pair_ab), against one block per tile:
+// flat buffers at K = 16 / 64 +7.8% / +2.5%, chunk-list state_dicts +3.0%,
+// the rows kernel (cfg2 landed) +3.5%, the K = 256 cfg3 planes +1.1% (late
+// claims; with early ones the K = 256 planes lost up to 2%, and the queue
+// stopped at K = 128 for a while).  (Process-level A/Bs had credited the
+// queue with +3% at K = 256 and debited the rows kernel 1%: the first
+// process of a pair ran faster whichever build it was,
 // profiles/r06/queue_ab/README.md.)  An A/B build may set P2P_SPLIT_QUEUE 0
 // (no queue at all).
 #ifndef P2P_SPLIT_QUEUE
@@ -774,7 +781,7 @@ static void launch_flat(const float* const* peers, int K, const int32_t* k_dev, 
                         float lr, hipStream_t stream, bool recip = false, bool share = false) {
   int64_t done = 0;
   {
-    const int64_t tiles = split_tiles_for(K, n / kSTile, use_queue<kFlat>(share, k_dev, K));
+    const int64_t tiles = split_tiles_for(K, n / kSTile, use_queue<kFlat>(share, k_dev, K) && K <= kAllTilesMaxK);
     if (tiles > 0) {
       launch_split<kFlat>(peers, K, k_dev, tiles, w, out, lr, nullptr, nullptr, nullptr, recip, stream, share);
       done = tiles * kSTile;
