@@ -90,13 +90,15 @@ int64_t p2p_tile_elems(int32_t rule, int32_t k);
  *   acc = +0 (:15); acc += peers[j] for j in list order (:25-28);
  *   acc /= K (:31-32); w += fp32(lr) * acc (:36-38, lr = 0.1 there).
  * Kernel choice (a pure function of k and n, same bits either way): for
- * k >= 16, every whole 8192-float tile (from one round of the CU count up)
- * runs on the LDS-DMA split kernel (loader + consumer waves; a persistent
- * grid of one block per CU claiming tiles from a counter pair of a
- * device-global ring, which each launch leaves zeroed), the < 8192-float
- * tail on the VGPR kernel; under P2P_HINT_SHARE_CUS (p2p_aggregate_ex_f32)
- * and on the device-K path the split kernel runs one block per tile over
- * whole rounds of tiles and the VGPR kernel the rest.  The peer pointers
+ * 16 <= k <= 128, every whole 8192-float tile (from one round of the CU
+ * count up) runs on the LDS-DMA split kernel (loader + consumer waves; a
+ * persistent grid of one block per CU claiming tiles from a counter pair of
+ * a device-global ring, which each launch leaves zeroed), the < 8192-float
+ * tail on the VGPR kernel; for 129 <= k <= 256 whole rounds of tiles run on
+ * the same queued kernel, the rest on the VGPR kernel; above 256, under
+ * P2P_HINT_SHARE_CUS (p2p_aggregate_ex_f32) and on the device-K path the
+ * split kernel runs one block per tile over whole rounds of tiles and the
+ * VGPR kernel the rest.  The peer pointers
  * are read from device memory each launch; 4-byte-aligned (not 16-byte)
  * pointers are handled, more slowly. */
 int32_t p2p_fedavg_apply_f32(const float *const *peers, int32_t k, int64_t n, float *w, float lr,
@@ -134,8 +136,8 @@ int32_t p2p_aggregate_f32(const float *const *peers, int32_t k, int64_t n, int32
  * -- the all-gather of a sharded round (p2pdl_amd/sharded.py PeerPlanes,
  * SURVEY.md §8(e)).  The FedAvg split kernel then runs one block per tile,
  * so each tile's end frees a CU the dispatcher can hand to that kernel,
- * instead of its persistent tile-queue grid, which holds every CU until the
- * launch ends.  Same results either way; unknown hint bits are
+ * instead of its persistent tile-queue grid (8 <= k <= 256), which holds
+ * every CU until the launch ends.  Same results either way; unknown hint bits are
  * P2P_ERR_INVALID. */
 #define P2P_HINT_SHARE_CUS 1
 int32_t p2p_aggregate_ex_f32(const float *const *peers, int32_t k, int64_t n, int32_t rule, int32_t trim_b,
