@@ -255,6 +255,36 @@ def test_split_kernel_share_cus_hint_same_bits(cuda):
         assert_bits_equal(got[1][0][:9000], w_ref, what=f"{rule} w vs oracle")
 
 
+def test_split_kernel_queue_random_launches(cuda):
+    """The tile queue under churn: 24 launches with random K (8..256, both
+    claim schedules' ranges, whole rounds and every-whole-tile plans) and
+    random sizes around CU-round edges, alternating over three streams
+    without synchronising in between, every mean checked on windows at both
+    ends and around the split / VGPR boundary against the oracle."""
+    rng = np.random.default_rng(0x51EE)
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    streams = [torch.cuda.Stream(cuda) for _ in range(3)]
+    cases = []
+    for i in range(24):
+        k = int(rng.choice([8, 9, 16, 31, 64, 100, 128, 129, 200, 256]))
+        n = int(rng.integers(1, 3) * cus * SPLIT_TILE + rng.integers(0, 3 * SPLIT_TILE))
+        if k * n * 4 > (3 << 30):
+            n = cus * SPLIT_TILE + int(rng.integers(0, SPLIT_TILE))
+        seed = 0x9000 + i
+        rows, _ = split_case(cuda, k, n, seed, pitch_pad=64)
+        out = torch.full((n,), float("nan"), dtype=torch.float32, device=cuda)
+        cases.append((k, n, seed, rows, out))
+    torch.cuda.synchronize()
+    for i, (k, n, seed, rows, out) in enumerate(cases):
+        with torch.cuda.stream(streams[i % 3]):
+            ops.aggregate(rows, "fedavg", out=out)
+    torch.cuda.synchronize()
+    for k, n, seed, rows, out in cases:
+        got = host(out)
+        for a, b in split_windows(n, cus):
+            assert_bits_equal(got[a:b], split_expect(k, seed, a, b)[1], what=f"K={k} n={n} [{a}, {b})")
+
+
 def test_fedavg_split_kernel_unaligned_rows_and_mean_only(cuda):
     """Rows 4-B but not 16-B aligned: the split kernel's element-wise path,
     same bits; then the mean alone (no w) through the DMA path."""

@@ -1,0 +1,48 @@
+"""CPU checks of the host-side launch plans of the FedAvg split kernel
+(p2pdl_amd/ops.py): the chunk list of a state_dict of separately allocated
+tensors (include/p2pdl.h p2p_fedavg_split_chunks_f32) and the route switch.
+No GPU: the library's plan helper reads the CU count from the device when
+there is one and falls back to 256 otherwise; the pointers are synthetic."""
+import numpy as np
+import pytest
+
+from p2pdl_amd import _native as N
+from p2pdl_amd import ops
+
+CUS = 256  # p2p_fedavg_split_plan's fallback without a device
+
+
+def _ptrs(L, K, base=1 << 30):
+    return (np.arange(L * K, dtype=np.uint64).reshape(L, K) * np.uint64(1 << 22)) + np.uint64(base)
+
+
+def test_chunk_plan_layout():
+    if int(N.lib().p2p_fedavg_split_plan(16, CUS)) != CUS:
+        pytest.skip("a device with another CU count is visible")
+    n = np.array([1_234_567, 3, 0, 8 * 1024 * CUS], dtype=np.int64)
+    ptrs = _ptrs(4, 16)
+    mask, lst = ops._chunk_plan(ptrs, [1 << 24] * 4, None, n, 16, 0)
+    assert list(mask) == [True, True, False, True]  # an empty key takes no chunk
+    nch = [-(-int(m) // 1024) if m else 0 for m in n]
+    C = sum(nch)
+    assert len(lst) == 8 * -(-C // 8) and lst.dtype == ops._SPLIT_DTYPE
+    assert (lst["seg"][:nch[0]] == 0).all() and (lst["c0"][:nch[0]] == np.arange(nch[0]) * 1024).all()
+    assert lst["seg"][nch[0]] == 1 and lst["c0"][nch[0]] == 0
+    assert (lst["seg"][nch[0] + 1:C] == 3).all() and (lst["seg"][C:] == -1).all() and (lst["c0"][C:] == 0).all()
+
+
+def test_chunk_plan_declines():
+    n = np.array([8 * 1024 * CUS], dtype=np.int64)
+    ptrs = _ptrs(1, 16)
+    assert ops._chunk_plan(ptrs, [1 << 24], None, n, 15, 0) is None            # K < 16
+    assert ops._chunk_plan(ptrs, [1 << 24], None, n, 16, ops.P2P_RULE_MEDIAN) is None  # a robust rule
+    assert ops._chunk_plan(ptrs, [1 << 24], None, np.array([1024 * 100]), 16, 0) is None  # under a CU round
+    odd = ptrs.copy()
+    odd[0, 5] += np.uint64(4)  # one peer view 4-B aligned only: no chunked key left
+    assert ops._chunk_plan(odd, [1 << 24], None, n, 16, 0) is None
+    assert ops._chunk_plan(ptrs, [(1 << 24) + 8], None, n, 16, 0) is None      # w 8-B aligned
+    assert ops._chunk_plan(ptrs, [1 << 24], [(1 << 24) + 4], n, 16, 0) is None  # out 4-B aligned
+
+
+def test_state_dict_route_is_checked():
+    assert ops.STATE_DICT_ROUTE == "chunks"  # the product route
