@@ -351,18 +351,25 @@ def _chunk_plan(ptrs: np.ndarray, w_ptrs, out_ptrs, n_arr: np.ndarray, K: int, r
 STATE_DICT_ROUTE = "chunks"
 
 
-def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_frac, outs, dev, cache_key=None):
-    r = rule_id(rule)
-    if r not in FEDAVG_RULES and K > MAX_ROBUST_PEERS:
-        raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {K}")
-    b = trim_count(K, trim_frac) if (r == P2P_RULE_TRIMMED and trim_b is None) else int(trim_b or 0)
-    tile = int(N.lib().p2p_tile_elems(r, K))
-    L = len(ws)
-    n_arr = np.asarray(numels, dtype=np.int64)
-    w_ptrs = [w.data_ptr() for w in ws]
-    out_ptrs = [o.data_ptr() for o in outs] if outs is not None else None
-    ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
-    route = STATE_DICT_ROUTE
+class _Layout:
+    """Everything of a segment-table launch but its addresses: the plan (the
+    chunk list / split tile list, which keys and ranges the VGPR kernel
+    takes), the byte layout of the one device buffer and a host image with
+    every address-independent field filled.  A pure function of (element
+    counts, K, rule, trim, outs or not, route, the keys' 16-B alignment), so
+    a round whose updates arrive at new addresses -- every round of a node
+    whose listener unpickles them (node/node.py:138-141) -- reuses it and
+    only writes the addresses (_LAYOUTS)."""
+
+    __slots__ = ("tiles", "r", "b", "rem_idx", "start4", "offs", "template", "has_plan", "split", "full_rows",
+                 "rem_rows", "Lr")
+
+
+_LAYOUTS: "OrderedDict[tuple, _Layout]" = OrderedDict()
+_LAYOUTS_MAX = 32
+
+
+def _build_layout(ptrs, w_ptrs, out_ptrs, n_arr, K, r, b, tile, route):
     plan = chunks = None
     if route == "chunks":
         chunks = _chunk_plan(ptrs, w_ptrs, out_ptrs, n_arr, K, r)
@@ -370,6 +377,7 @@ def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_fra
         plan = _split_plan(ptrs, w_ptrs, out_ptrs, n_arr, K, r)
     elif route != "vgpr":
         raise ValueError(f"unknown STATE_DICT_ROUTE {route!r}")
+    L = len(n_arr)
     # The table the VGPR segment kernel runs: every segment, or -- with a
     # split plan -- what the split kernel leaves of each (its tail past the
     # taken whole tiles), as segments of their own whose peer rows, w and out
@@ -385,50 +393,98 @@ def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_fra
         start = taken * SPLIT_TILE
         rem_idx = np.nonzero(n_arr - start > 0)[0]
         start = start[rem_idx]
-    Lr = len(rem_idx)
+    lay = _Layout()
+    lay.r, lay.b = r, b
+    lay.Lr = Lr = len(rem_idx)
+    lay.rem_idx, lay.start4 = rem_idx, start.astype(np.uint64) * np.uint64(4)
     rem = np.zeros(Lr, dtype=_SEG_DTYPE)
-    rem["w"] = np.asarray(w_ptrs, dtype=np.uint64)[rem_idx] + start.astype(np.uint64) * np.uint64(4)
-    if outs is not None:
-        rem["out"] = np.asarray(out_ptrs, dtype=np.uint64)[rem_idx] + start.astype(np.uint64) * np.uint64(4)
     rem["n"] = n_arr[rem_idx] - start
     t_arr = -(-rem["n"] // tile)
     if Lr:
         rem["tile_begin"][1:] = np.cumsum(t_arr)[:-1]
-    tiles = int(t_arr.sum())
-    rem_ptrs = ptrs[rem_idx] + (start.astype(np.uint64) * np.uint64(4))[:, None]
-    if tiles == 0 and plan is None:
-        return
+    lay.tiles = int(t_arr.sum())
+    lay.has_plan = plan is not None
+    if lay.tiles == 0 and plan is None:
+        lay.template = None  # nothing to launch
+        return lay
     # one device buffer: [the full table (split kernel's segments)] [the
     # remainder table] [split tile list] [full peer rows] [remainder peer
-    # rows].  Its tables hold device addresses inside itself: allocate it
-    # first, then fill the host image with those addresses and copy it once.
+    # rows].  Its tables hold device addresses inside itself: the launch
+    # allocates it first, then writes those addresses into a copy of the
+    # template and copies it once.
     full = np.zeros(L if plan is not None else 0, dtype=_SEG_DTYPE)
     lst = plan[1] if plan is not None else np.zeros(0, dtype=_SPLIT_DTYPE)
-    parts = [full.nbytes, rem.nbytes, lst.nbytes, 8 * K * len(full), rem_ptrs.nbytes]
+    parts = [full.nbytes, rem.nbytes, lst.nbytes, 8 * K * len(full), 8 * K * Lr]
     offs = np.concatenate([[0], np.cumsum(parts)]).astype(np.int64)
-    host = np.empty(int(offs[-1]), dtype=np.uint8)
-    buf = torch.empty(host.nbytes, dtype=torch.uint8, device=dev)
-    base = buf.data_ptr()
+    lay.offs = [int(x) for x in offs]
+    host = np.zeros(lay.offs[-1], dtype=np.uint8)
     if plan is not None:
-        full["w"] = w_ptrs
-        if outs is not None:
-            full["out"] = out_ptrs
         full["n"] = n_arr
-        full["peers"] = np.uint64(base + offs[3]) + np.arange(L, dtype=np.uint64) * np.uint64(8 * K)
         host[offs[0]:offs[1]] = full.view(np.uint8)
         host[offs[2]:offs[3]] = lst.view(np.uint8)
-        host[offs[3]:offs[4]] = ptrs.view(np.uint8).reshape(-1)
-    rem["peers"] = np.uint64(base + offs[4]) + np.arange(Lr, dtype=np.uint64) * np.uint64(8 * K)
     host[offs[1]:offs[2]] = rem.view(np.uint8)
-    host[offs[4]:offs[5]] = rem_ptrs.view(np.uint8).reshape(-1)
-    _RING.to_device(host, dev, out=buf)
+    lay.template = host
+    lay.full_rows = np.uint64(offs[3]) + np.arange(len(full), dtype=np.uint64) * np.uint64(8 * K)
+    lay.rem_rows = np.uint64(offs[4]) + np.arange(Lr, dtype=np.uint64) * np.uint64(8 * K)
     if plan is None:
-        split = None
+        lay.split = None
     elif chunks is not None:  # the chunk list: ntiles * 8 entries
-        split = (int(offs[2]), len(lst) // (SPLIT_TILE // ROW_CHUNK), int(offs[0]), "chunks")
+        lay.split = (lay.offs[2], len(lst) // (SPLIT_TILE // ROW_CHUNK), lay.offs[0], "chunks")
     else:
-        split = (int(offs[2]), len(lst), int(offs[0]), "tiles")
-    entry = (buf, tiles, r, b, torch.cuda.current_stream(dev).cuda_stream, (int(offs[1]), Lr, split))
+        lay.split = (lay.offs[2], len(lst), lay.offs[0], "tiles")
+    return lay
+
+
+def _launch_segments(ws, ptrs: np.ndarray, numels, rule, K, lr, trim_b, trim_frac, outs, dev, cache_key=None):
+    r = rule_id(rule)
+    if r not in FEDAVG_RULES and K > MAX_ROBUST_PEERS:
+        raise ValueError(f"robust rules support at most {MAX_ROBUST_PEERS} peers, got {K}")
+    b = trim_count(K, trim_frac) if (r == P2P_RULE_TRIMMED and trim_b is None) else int(trim_b or 0)
+    n_arr = np.asarray(numels, dtype=np.int64)
+    w_arr = np.fromiter((w.data_ptr() for w in ws), dtype=np.uint64, count=len(ws))
+    out_arr = np.fromiter((o.data_ptr() for o in outs), dtype=np.uint64, count=len(outs)) if outs is not None else None
+    ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+    route = STATE_DICT_ROUTE
+    mask = None  # the keys' 16-B alignment, where a split plan depends on it
+    if route != "vgpr" and r in FEDAVG_RULES and K >= 16 and len(n_arr):
+        low = np.bitwise_or.reduce(ptrs, axis=1) | w_arr
+        if out_arr is not None:
+            low |= out_arr
+        mask = ((low & np.uint64(15)) == 0).tobytes()
+    lkey = (dev.index, n_arr.tobytes(), K, r, b, out_arr is not None, route, mask)
+    with _TABLES_LOCK:
+        lay = _LAYOUTS.get(lkey)
+        if lay is not None:
+            _LAYOUTS.move_to_end(lkey)
+    if lay is None:
+        lay = _build_layout(ptrs, w_arr, out_arr, n_arr, K, r, b, int(N.lib().p2p_tile_elems(r, K)), route)
+        with _TABLES_LOCK:
+            _LAYOUTS[lkey] = lay
+            while len(_LAYOUTS) > _LAYOUTS_MAX:
+                _LAYOUTS.popitem(last=False)
+    if lay.template is None:
+        return None
+    o = lay.offs
+    host = lay.template.copy()
+    buf = torch.empty(host.nbytes, dtype=torch.uint8, device=dev)
+    base = np.uint64(buf.data_ptr())
+    if lay.has_plan:
+        full = host[o[0]:o[1]].view(_SEG_DTYPE)
+        full["w"] = w_arr
+        if out_arr is not None:
+            full["out"] = out_arr
+        full["peers"] = base + lay.full_rows
+        host[o[3]:o[4]] = ptrs.view(np.uint8).reshape(-1)
+    if lay.Lr:
+        rem = host[o[1]:o[2]].view(_SEG_DTYPE)
+        ri = lay.rem_idx
+        rem["w"] = w_arr[ri] + lay.start4
+        if out_arr is not None:
+            rem["out"] = out_arr[ri] + lay.start4
+        rem["peers"] = base + lay.rem_rows
+        host[o[4]:o[5]] = (ptrs[ri] + lay.start4[:, None]).view(np.uint8).reshape(-1)
+    _RING.to_device(host, dev, out=buf)
+    entry = (buf, lay.tiles, r, b, torch.cuda.current_stream(dev).cuda_stream, (o[1], lay.Lr, lay.split))
     with torch.cuda.device(dev):
         _launch_entry(entry, K, lr, N.stream_handle())
     if cache_key is not None:
