@@ -132,10 +132,11 @@ def parse():
     ap.add_argument("--coords", type=int, default=0, help="override coordinates per GPU")
     ap.add_argument("--peers", type=int, default=0, help="override K")
     ap.add_argument("--chunks", type=int, default=8, help="all-gather pipeline chunks per rank (N>1)")
-    ap.add_argument("--gather", default="overlap", choices=["overlap", "inline"],
+    ap.add_argument("--gather", default="overlap", choices=list(GATHER_LEGS),
                     help="N>1: each plane's all-gather on a second stream beside the next plane's reduction "
-                         "(the product, sharded.PeerPlanes.aggregate_gather_) or in line on the compute stream; "
-                         "the default run also times the other leg (config.gather_legs)")
+                         "(the product, sharded.PeerPlanes.aggregate_gather_), in line on the compute stream, "
+                         "or p2p: overlapped, as a direct exchange (sharded.exchange_: grouped send/recv to "
+                         "every peer at once); the default run also times the other legs (config.gather_legs)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--sub-cpu-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -243,6 +244,10 @@ def pitched_slab(K, S, C, dev):
     return torch.empty((K, S, -(-C // PITCH) * PITCH), dtype=torch.float32, device=dev)
 
 
+# --gather legs: (exchange on a second stream?, sharded.EXCHANGES kind)
+GATHER_LEGS = {"overlap": (True, "all_gather"), "inline": (False, "all_gather"), "p2p": (True, "p2p")}
+
+
 def pipeline_summary(rank: int, kernel_ms, gather_ms, wall_ms: float, gather_bytes, world: int) -> dict:
     """One rank's reduce / all-gather pipeline over a step (or a job): the
     per-plane kernel and all-gather times (ms, HIP events on their own
@@ -329,8 +334,8 @@ def measure_flat(c: Ctx, args, name, rule, K, n, seed, steps, warmup, cpu_s, chu
             ev[(s, phase)] = e
 
         planes.aggregate_gather_(wviews, w_full, rule=rule, lr=0.1,
-                                 comm=comm if world > 1 and gather == "overlap" else None,
-                                 hook=hook if record else None)
+                                 comm=comm if world > 1 and GATHER_LEGS[gather][0] else None,
+                                 hook=hook if record else None, exchange=GATHER_LEGS[gather][1])
         if record:
             end = torch.cuda.Event(enable_timing=True)
             end.record(comp)  # after the compute stream waited for the last all-gather
@@ -528,7 +533,8 @@ def measure_cfg3_full(c: Ctx, args, passes=2, chunks=8, gather="overlap"):
             # tile u is the global range [u*T*N, (u+1)*T*N)
             tile_full = w_full[u * T * world:(u + 1) * T * world] if world > 1 else None
             planes.aggregate_gather_(wviews, tile_full, rule="fedavg", lr=0.1,
-                                     comm=comm if world > 1 and gather == "overlap" else None, hook=hook)
+                                     comm=comm if world > 1 and GATHER_LEGS[gather][0] else None, hook=hook,
+                                     exchange=GATHER_LEGS[gather][1])
             end = torch.cuda.Event(enable_timing=True)
             end.record(comp)
             torch.cuda.synchronize()
@@ -1660,8 +1666,8 @@ def scale_plan(world: int, n1: dict, *, steps: int = 10, warmup: int = 2, chunks
         step_ms * tiles
     fill_s = (K + 1) * n * 4 / (fill_tbs * 1e12)
     total_s = startup_s + fill_s + (steps + warmup) * step_pred / 1e3 + 2 * tiles * (fill_s + job_ms / 1e3)
-    if world > 1:  # the other all-gather leg (config.gather_legs): in line, 1 + min(steps, 5) steps
-        total_s += fill_s + (1 + min(steps, 5)) * (step_ms + gather_ms) / 1e3
+    if world > 1:  # the other exchange legs (config.gather_legs), 1 + min(steps, 5) steps each, priced in line
+        total_s += (len(GATHER_LEGS) - 1) * (fill_s + (1 + min(steps, 5)) * (step_ms + gather_ms) / 1e3)
     return {"world": world, "bytes_per_rank": max(main_bytes, full_bytes), "fits_hbm": max(main_bytes, full_bytes)
             < 0.97 * HBM_BYTES, "step_ms": round(step_pred, 3), "allgather_ms_per_step": round(gather_ms, 3),
             "seconds": round(total_s, 1)}
@@ -1776,16 +1782,25 @@ def main():
                                             args.cpu_seconds, args.chunks, gather=args.gather)
             step_ms = step_s * 1e3
             if world > 1 and not args.no_sub:
-                # the other all-gather leg, same data and plan, fewer steps:
-                # one driver run carries both
-                other = "inline" if args.gather == "overlap" else "overlap"
-                o_rec, o_s = measure_flat(c, args, args.workload, rule, K, n, seed, min(args.steps, 5), 1, 0,
-                                          args.chunks, gather=other)
-                main_rec["config"]["gather_legs"] = {
-                    args.gather: {"ms_per_step": round(step_ms, 4), "value": main_rec["value"],
-                                  "pipeline": main_rec["config"].get("pipeline")},
-                    other: {"ms_per_step": o_rec["ms_per_step"], "value": o_rec["value"],
-                            "pipeline": o_rec["config"].get("pipeline"), "per_rank": o_rec["config"].get("per_rank")}}
+                # the other exchange legs, same data and plan, fewer steps:
+                # one driver run carries all three (VERDICT r05 next #4 and
+                # weak #7: in line, overlapped, and the direct exchange)
+                legs = {args.gather: {"ms_per_step": round(step_ms, 4), "value": main_rec["value"],
+                                      "pipeline": main_rec["config"].get("pipeline")}}
+                for other in GATHER_LEGS:
+                    if other == args.gather:
+                        continue
+                    try:
+                        o_rec, o_s = measure_flat(c, args, args.workload, rule, K, n, seed, min(args.steps, 5), 1,
+                                                  0, args.chunks, gather=other)
+                    except (RuntimeError, dist.DistBackendError) as e:  # a leg's failure is its record, not the line's
+                        legs[other] = {"error": f"{type(e).__name__}: {e}"[:300]}
+                        torch.cuda.synchronize()
+                        continue
+                    legs[other] = {"ms_per_step": o_rec["ms_per_step"], "value": o_rec["value"],
+                                   "pipeline": o_rec["config"].get("pipeline"),
+                                   "per_rank": o_rec["config"].get("per_rank")}
+                main_rec["config"]["gather_legs"] = legs
         steps = main_rec["steps"]
         sub = {}
         if not args.no_sub and args.workload == "cfg3" and not (args.coords or args.peers):

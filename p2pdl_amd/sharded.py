@@ -43,6 +43,53 @@ DEFAULT_CHUNK = 16 * 1024 * 1024  # coordinates per chunk (64 MB of fp32)
 PLANE_BYTES = 16 << 30
 ROW_ALIGN = 64  # fp32 elements: every peer row of a plane starts a 256-B boundary
 
+# How a round's pieces reach every rank:
+#   all_gather  one RCCL all_gather_into_tensor (its rings over xGMI);
+#   p2p         a direct exchange -- this rank's piece sent to each of the
+#               G-1 others and theirs received, as one grouped batch of
+#               send/recv pairs (dist.batch_isend_irecv: on RCCL one group
+#               call, every peer pair on its own xGMI link at once).
+# Same bytes into the same places; which is faster on a node is the
+# measurement bench.py's N > 1 line carries (config.gather_legs).
+EXCHANGES = ("all_gather", "p2p")
+
+
+def exchange_(out: torch.Tensor, mine: torch.Tensor, group=None, exchange: str = "all_gather") -> None:
+    """out (G equal pieces, rank order) <- every rank's ``mine``, on the
+    current stream.  ``mine`` may be this rank's own piece of ``out`` (in
+    place) or a separate tensor of the same length."""
+    if exchange == "all_gather":
+        dist.all_gather_into_tensor(out, mine, group=group)
+        return
+    if exchange != "p2p":
+        raise ValueError(f"exchange must be one of {EXCHANGES}, got {exchange!r}")
+    G, r, C = dist.get_world_size(group), dist.get_rank(group), mine.numel()
+    if out.numel() != G * C:
+        raise ValueError(f"out has {out.numel()} elements for {G} pieces of {C}")
+    if out.is_cuda and G > 1 and dist.get_backend(group) == "gloo":
+        # gloo's send/recv move host memory only: the one-GPU rehearsal
+        # (ranks sharing a card) stages through the host
+        h_out = torch.empty(out.numel(), dtype=out.dtype)
+        exchange_(h_out, mine.cpu(), group, "p2p")
+        out.copy_(h_out)
+        return
+    own = out[r * C:(r + 1) * C]
+    if own.data_ptr() != mine.data_ptr():
+        own.copy_(mine)
+    if G == 1:
+        return
+
+    def glob(q):
+        return q if group is None else dist.get_global_rank(group, q)
+
+    ops_ = []
+    for d in range(1, G):  # distance d: send to r+d, receive from r-d (every pair matched)
+        to, frm = (r + d) % G, (r - d) % G
+        ops_.append(dist.P2POp(dist.isend, mine, glob(to), group))
+        ops_.append(dist.P2POp(dist.irecv, out[frm * C:(frm + 1) * C], glob(frm), group))
+    for req in dist.batch_isend_irecv(ops_):
+        req.wait()
+
 
 def plane_count(k: int, n: int, at_least: int = 1) -> int:
     """Chunks S >= at_least that split n coordinates evenly (n % S == 0) into
@@ -135,7 +182,8 @@ class PeerPlanes:
 
     def aggregate_gather_(self, ws: Sequence[torch.Tensor], w_full: torch.Tensor | None = None, *,
                           rule="fedavg", lr: float = 0.1, trim_frac: float = 0.2, group=None,
-                          comm=None, reduce: Callable | None = None, hook: Callable | None = None) -> None:
+                          comm=None, reduce: Callable | None = None, hook: Callable | None = None,
+                          exchange: str = "all_gather") -> None:
         """One aggregation round over every plane.  ``ws[s]`` is this rank's
         chunk s of w -- global coordinates ``global_range(s, rank, G)``, which
         for equal planes is global chunk s*G + rank (ChunkPlan's round robin)
@@ -148,7 +196,10 @@ class PeerPlanes:
         copied to w_full[o, o+C).  ``hook(s, phase, stream)`` runs at "reduce0" /
         "reduce1" / "gather0" / "gather1" on the stream of that step (timing
         events); ``reduce(planes, s, w, rule, lr, trim_frac)`` replaces the HIP
-        reduction (the CPU gloo tests)."""
+        reduction (the CPU gloo tests); ``exchange`` picks the all-gather or
+        the direct exchange (``EXCHANGES``)."""
+        if exchange not in EXCHANGES:
+            raise ValueError(f"exchange must be one of {EXCHANGES}, got {exchange!r}")
         if len(ws) != self.chunks:
             raise ValueError(f"{len(ws)} w chunks for {self.chunks} planes")
         gather = w_full is not None and dist.is_initialized()
@@ -181,13 +232,13 @@ class PeerPlanes:
                 with torch.cuda.stream(comm):
                     if hook:
                         hook(s, "gather0", comm)
-                    dist.all_gather_into_tensor(out, ws[s], group=group)
+                    exchange_(out, ws[s], group, exchange)
                     if hook:
                         hook(s, "gather1", comm)
             else:
                 if hook:
                     hook(s, "gather0", comp)
-                dist.all_gather_into_tensor(out, ws[s].contiguous().clone(), group=group)
+                exchange_(out, ws[s].contiguous().clone(), group, exchange)
                 if hook:
                     hook(s, "gather1", comp)
         if gather and comm is not None:
@@ -247,14 +298,19 @@ def _default_reduce(peers, w, rule, lr, trim_frac, share_cus=False):
 
 def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor], *, rule="fedavg",
                        lr: float = 0.1, trim_frac: float = 0.2, chunk: int = DEFAULT_CHUNK,
-                       group=None, reduce: Callable | None = None, overlap: bool = True) -> ChunkPlan:
+                       group=None, reduce: Callable | None = None, overlap: bool = True,
+                       exchange: str = "all_gather") -> ChunkPlan:
     """w_full += lr * rule(peers) with the coordinates split across ranks.
 
     Every rank holds the full w and the full peer buffers (replicated inputs);
     each reduces its owned chunks in place, then all-gathers so every rank
     ends with the identical global model -- byte-identical to one GPU.
     ``reduce(peers, w, rule, lr, trim_frac)`` defaults to the HIP kernels;
-    tests substitute the CPU oracle to exercise the plan over gloo."""
+    tests substitute the CPU oracle to exercise the plan over gloo;
+    ``exchange`` picks how each round's chunks travel (``EXCHANGES``; the
+    ragged tail's small staging gather is always an all-gather)."""
+    if exchange not in EXCHANGES:
+        raise ValueError(f"exchange must be one of {EXCHANGES}, got {exchange!r}")
     gather = dist.is_initialized()  # a world of 1 still gathers (in place): the same call path
     world = dist.get_world_size(group) if gather else 1
     rank = dist.get_rank(group) if gather else 0
@@ -283,9 +339,9 @@ def sharded_aggregate_(w_full: torch.Tensor, peers_full: Sequence[torch.Tensor],
             ev.record(comp)
             comm.wait_event(ev)
             with torch.cuda.stream(comm):
-                dist.all_gather_into_tensor(out, mine, group=group)
+                exchange_(out, mine, group, exchange)
         else:
-            dist.all_gather_into_tensor(out, mine.clone(), group=group)
+            exchange_(out, mine.clone(), group, exchange)
     if plan.tail:
         st, ln = plan.tail_range(rank)
         if ln:

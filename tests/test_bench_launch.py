@@ -121,7 +121,14 @@ def test_gather_switch_parses():
     try:
         _sys.argv = ["bench.py", "--gpus", "2", "--gather", "inline"]
         assert bench.parse().gather == "inline"
+        _sys.argv = ["bench.py", "--gpus", "2", "--gather", "p2p"]
+        assert bench.parse().gather == "p2p"
         _sys.argv = ["bench.py"]
         assert bench.parse().gather == "overlap"
+        # every leg maps to a stream policy and one of sharded's exchanges
+        from p2pdl_amd import sharded
+
+        assert set(bench.GATHER_LEGS) == {"overlap", "inline", "p2p"}
+        assert all(ex in sharded.EXCHANGES for _, ex in bench.GATHER_LEGS.values())
     finally:
         _sys.argv = saved

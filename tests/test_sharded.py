@@ -129,27 +129,31 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, n, k, rule, chunk, q):
+def _worker(rank, world, port, n, k, rule, chunk, q, exchange="all_gather"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         peers = [torch.from_numpy(oracle.synth(n, 17, p, 1e-2)) for p in range(k)]
         w = torch.from_numpy(oracle.synth(n, 17, 0xFFFFF, 5e-2))
-        sharded_aggregate_(w, peers, rule=rule, chunk=chunk, reduce=oracle_reduce)
+        sharded_aggregate_(w, peers, rule=rule, chunk=chunk, reduce=oracle_reduce, exchange=exchange)
         q.put((rank, w.numpy().tobytes()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rule,n,k,chunk", [(2, "fedavg", 10_007, 5, 1000), (2, "fedavg", 4096, 3, 512),
-                                                  (2, "median", 3001, 7, 256), (2, "trimmed", 777, 10, 100),
-                                                  # the driver's 4-rank leg and an odd world, rehearsed on gloo
-                                                  (4, "fedavg", 10_007, 6, 300), (3, "median", 2049, 9, 128)])
-def test_gloo_world_byte_identical_to_single(world, rule, n, k, chunk):
+@pytest.mark.parametrize("world,rule,n,k,chunk,exchange", [
+    (2, "fedavg", 10_007, 5, 1000, "all_gather"), (2, "fedavg", 4096, 3, 512, "all_gather"),
+    (2, "median", 3001, 7, 256, "all_gather"), (2, "trimmed", 777, 10, 100, "all_gather"),
+    # the driver's 4-rank leg and an odd world, rehearsed on gloo
+    (4, "fedavg", 10_007, 6, 300, "all_gather"), (3, "median", 2049, 9, 128, "all_gather"),
+    # the direct exchange (sharded.exchange_): same bytes, same places
+    (2, "fedavg", 10_007, 5, 1000, "p2p"), (3, "fedavg", 10_007, 6, 300, "p2p"), (4, "trimmed", 2049, 9, 128, "p2p")])
+def test_gloo_world_byte_identical_to_single(world, rule, n, k, chunk, exchange):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, k, rule, chunk, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, k, rule, chunk, q, exchange))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=120) for _ in procs)
@@ -166,7 +170,7 @@ def test_gloo_world_byte_identical_to_single(world, rule, n, k, chunk):
     assert all(got[r] == want.tobytes() for r in range(world))
 
 
-def _planes_worker(rank, world, port, n, k, rule, S, q):
+def _planes_worker(rank, world, port, n, k, rule, S, q, exchange="all_gather"):
     """Memory-sharded inputs: this rank holds only its owned chunks of every
     peer, in PeerPlanes (CPU tensors here; the oracle reduces), and one
     aggregate_gather_ reassembles the global model."""
@@ -190,19 +194,23 @@ def _planes_worker(rank, world, port, n, k, rule, S, q):
             oracle_reduce([pl.row(s, p) for p in range(pl.k)], wchunk, rule_, lr, trim_frac)
 
         seen = []
-        planes.aggregate_gather_(ws, w_full, rule=rule, reduce=reduce, hook=lambda s, ph, st: seen.append((s, ph)))
+        planes.aggregate_gather_(ws, w_full, rule=rule, reduce=reduce, hook=lambda s, ph, st: seen.append((s, ph)),
+                                 exchange=exchange)
         assert seen == [(s, ph) for s in range(S) for ph in ("reduce0", "reduce1", "gather0", "gather1")]
         q.put((rank, w_full.numpy().tobytes()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rule,n,k,S", [(2, "fedavg", 2 * 3 * 1001, 5, 3), (2, "trimmed", 2 * 2 * 640, 10, 2)])
-def test_gloo_peer_planes_round_byte_identical_to_single(world, rule, n, k, S):
+@pytest.mark.parametrize("world,rule,n,k,S,exchange", [
+    (2, "fedavg", 2 * 3 * 1001, 5, 3, "all_gather"), (2, "trimmed", 2 * 2 * 640, 10, 2, "all_gather"),
+    (2, "fedavg", 2 * 3 * 1001, 5, 3, "p2p"), (4, "fedavg", 4 * 2 * 500, 3, 2, "p2p")])
+def test_gloo_peer_planes_round_byte_identical_to_single(world, rule, n, k, S, exchange):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_planes_worker, args=(r, world, port, n, k, rule, S, q)) for r in range(world)]
+    procs = [ctx.Process(target=_planes_worker, args=(r, world, port, n, k, rule, S, q, exchange))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=120) for _ in procs)
@@ -306,6 +314,14 @@ def _unequal_planes_rank(rank, world, port, k, sizes, n, q=None):
             dist.destroy_process_group()
 
 
+def test_exchange_refuses_an_unknown_kind():
+    planes = sharded.PeerPlanes(2, 1, 10, "cpu")
+    with pytest.raises(ValueError, match="exchange"):
+        planes.aggregate_gather_([torch.zeros(10)], reduce=lambda *a: None, exchange="ring")
+    with pytest.raises(ValueError, match="exchange"):
+        sharded_aggregate_(torch.zeros(10), [torch.zeros(10)], reduce=lambda *a: None, exchange="ring")
+
+
 def test_peer_planes_global_range_equal_planes_is_the_round_robin():
     """Equal planes: global_range(s, r, G) is ChunkPlan's global chunk s*G + r."""
     planes = sharded.PeerPlanes(2, 3, 10, "cpu")
@@ -327,7 +343,7 @@ def test_peer_planes_checks_round_shapes():
 
 
 # ---------------------------------------------------------------- GPU leg
-def _gpu_worker(rank, world, port, n, k, rule, chunk, overlap, q):
+def _gpu_worker(rank, world, port, n, k, rule, chunk, overlap, q, exchange="all_gather"):
     """One rank: the HIP reduce (the default of sharded_aggregate_) on cuda:0,
     gloo for the all-gather (both ranks share the one GPU of the test box;
     the driver's multi-GPU bench uses RCCL)."""
@@ -338,7 +354,7 @@ def _gpu_worker(rank, world, port, n, k, rule, chunk, overlap, q):
         torch.cuda.set_device(dev)
         peers = [torch.from_numpy(oracle.synth(n, 23, p, 1e-2)).to(dev) for p in range(k)]
         w = torch.from_numpy(oracle.synth(n, 23, 0xFFFFF, 5e-2)).to(dev)
-        plan = sharded_aggregate_(w, peers, rule=rule, chunk=chunk, overlap=overlap)
+        plan = sharded_aggregate_(w, peers, rule=rule, chunk=chunk, overlap=overlap, exchange=exchange)
         torch.cuda.synchronize()
         q.put((rank, w.cpu().numpy().tobytes(), plan.full_rounds, plan.tail))
         dist.barrier()
@@ -349,17 +365,19 @@ def _gpu_worker(rank, world, port, n, k, rule, chunk, overlap, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rule,n,k,chunk,overlap", [
-    ("fedavg", 100_003, 9, 8192, True),     # 6 full rounds + ragged tail, gather on a comm stream
-    ("fedavg", 65_536, 256, 16_384, False),  # no tail, K = 256
-    ("median", 50_001, 130, 4096, True),    # LDS-staged robust kernel (K > 128)
-    ("trimmed", 50_001, 64, 6000, True),    # one-lane robust kernel, unaligned chunk starts
-    ("trimmed", 30_011, 256, 4096, True),
-    ("median", 40_003, 256, 4096, True),    # the pair kernel (north-star median of 256)
-    ("median", 50_001, 128, 6000, True),    # cfg4's K, unaligned chunk starts
-    ("fedavg_torch_gpu", 70_001, 10, 6000, True),  # FedAvg as torch runs it on the GPU
+@pytest.mark.parametrize("rule,n,k,chunk,overlap,exchange", [
+    ("fedavg", 100_003, 9, 8192, True, "all_gather"),  # 6 full rounds + ragged tail, gather on a comm stream
+    ("fedavg", 100_003, 64, 8192, True, "p2p"),        # the direct exchange (host-staged on gloo)
+    ("median", 40_003, 256, 4096, False, "p2p"),
+    ("fedavg", 65_536, 256, 16_384, False, "all_gather"),  # no tail, K = 256
+    ("median", 50_001, 130, 4096, True, "all_gather"),    # LDS-staged robust kernel (K > 128)
+    ("trimmed", 50_001, 64, 6000, True, "all_gather"),    # one-lane robust kernel, unaligned chunk starts
+    ("trimmed", 30_011, 256, 4096, True, "all_gather"),
+    ("median", 40_003, 256, 4096, True, "all_gather"),    # the pair kernel (north-star median of 256)
+    ("median", 50_001, 128, 6000, True, "all_gather"),    # cfg4's K, unaligned chunk starts
+    ("fedavg_torch_gpu", 70_001, 10, 6000, True, "all_gather"),  # FedAvg as torch runs it on the GPU
 ])
-def test_gpu_world2_hip_reduce_byte_identical_to_oracle(cuda, rule, n, k, chunk, overlap):
+def test_gpu_world2_hip_reduce_byte_identical_to_oracle(cuda, rule, n, k, chunk, overlap, exchange):
     """VERDICT r01 missing #2: sharded_aggregate_ with the DEFAULT (HIP)
     per-shard reduce -- each rank reduces its round-robin chunks on the GPU,
     the all-gather reassembles -- byte-compared with the CPU oracle on both
@@ -367,7 +385,8 @@ def test_gpu_world2_hip_reduce_byte_identical_to_oracle(cuda, rule, n, k, chunk,
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, n, k, rule, chunk, overlap, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, n, k, rule, chunk, overlap, q, exchange))
+             for r in range(2)]
     for p in procs:
         p.start()
     got = {}
@@ -485,6 +504,12 @@ def _nccl_world1_worker(port, q):
         planes.aggregate_gather_(ws, w_full, rule="fedavg", comm=torch.cuda.Stream(dev))
         torch.cuda.synchronize()
         out["planes"] = (w_full.cpu().numpy().tobytes(), dist.get_backend())
+        # the direct exchange's call path (at world 1: the own piece only)
+        ws = [torch.from_numpy(w[s_ * C:(s_ + 1) * C].copy()).to(dev) for s_ in range(S)]
+        w_full.zero_()
+        planes.aggregate_gather_(ws, w_full, rule="fedavg", comm=torch.cuda.Stream(dev), exchange="p2p")
+        torch.cuda.synchronize()
+        out["planes_p2p"] = (w_full.cpu().numpy().tobytes(), dist.get_backend())
         q.put(out)
         dist.destroy_process_group()
     except BaseException as e:  # report, do not hang the parent
@@ -511,4 +536,6 @@ def test_gpu_world1_nccl_allgather_path(cuda):
         assert b == want.tobytes(), rule
     b, backend = got["planes"]
     peers = [oracle.synth(3 * 70_001, 37, p, 1e-2) for p in range(20)]
-    assert backend == "nccl" and b == oracle.fedavg(peers, oracle.synth(3 * 70_001, 37, 0xFFFFF, 5e-2))[0].tobytes()
+    want = oracle.fedavg(peers, oracle.synth(3 * 70_001, 37, 0xFFFFF, 5e-2))[0].tobytes()
+    assert backend == "nccl" and b == want
+    assert got["planes_p2p"] == (want, "nccl")
