@@ -4,7 +4,9 @@ table every call -- a round whose pickle.loads updates arrive at new
 addresses: aggregate_models over plain dicts of separately allocated
 tensors (ResNet-18 x 64), ops._TABLES cleared before each call, cProfile
 over the calls.  Measurement tool, not product.
-usage: python tools/prof_general.py [calls] [mlp]"""
+With "cached" the table is kept (the steady state of a round whose updates
+sit at the same addresses: the per-call host cost alone).
+usage: python tools/prof_general.py [calls] [mlp] [cached]"""
 import cProfile
 import io
 import os
@@ -24,7 +26,8 @@ from p2pdl_amd.aggregator import aggregation as agg  # noqa: E402
 
 def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 30
-    mlp = len(sys.argv) > 2 and sys.argv[2] == "mlp"  # cfg1: the MNIST MLP x 3
+    mlp = "mlp" in sys.argv[2:]  # cfg1: the MNIST MLP x 3
+    cached = "cached" in sys.argv[2:]
     dev = torch.device("cuda", 0)
     K = 3 if mlp else 64
     shapes = bench.MLP_SHAPES if mlp else bench.resnet18_param_shapes()
@@ -41,7 +44,8 @@ def main():
 
     def call():
         node.received_models.extend({"model": u, "sender": j} for j, u in enumerate(upd))
-        ops._TABLES.clear()
+        if not cached:
+            ops._TABLES.clear()
         agg.aggregate_models(node)
 
     for _ in range(3):
@@ -54,7 +58,13 @@ def main():
         call()
         torch.cuda.synchronize()
         t.append(time.perf_counter() - t0)
-    print(f"new table every call: median {np.median(t) * 1e6:.1f} us per call (host wall, synchronised)")
+    print(f"{'cached table' if cached else 'new table every call'}: median {np.median(t) * 1e6:.1f} us per call (host wall, synchronised)")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        call()
+    torch.cuda.synchronize()
+    print(f"back to back: {(time.perf_counter() - t0) / calls * 1e6:.1f} us per call (host wall, one sync at the end)")
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(calls):
