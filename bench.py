@@ -176,8 +176,12 @@ def roofline(alg_bytes: float, kern_ms: float, traffic, **extra) -> dict:
 
 def dist_info() -> dict:
     """What ran the exchange: the process group's world size and backend,
-    and the RCCL version torch was built against."""
-    info = {"world_size": dist.get_world_size(), "backend": dist.get_backend()}
+    the RCCL version torch was built against, and the RCCL settings the
+    environment gave it (NCCL_* / RCCL_*: channels, protocols, algorithms;
+    empty = RCCL's own defaults, the build's channel policy)."""
+    info = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+            "rccl_env": {k: v for k, v in sorted(os.environ.items())
+                         if k.startswith(("NCCL_", "RCCL_")) and "SOCKET" not in k}}
     try:
         v = torch.cuda.nccl.version()
         info["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
