@@ -335,11 +335,31 @@ def _chunk_plan(ptrs: np.ndarray, w_ptrs, out_ptrs, n_arr: np.ndarray, K: int, r
     ntiles = -(-C // (SPLIT_TILE // ROW_CHUNK))
     if ntiles == 0 or int(N.lib().p2p_fedavg_split_plan(K, ntiles)) <= 0:
         return None
-    M = ntiles * (SPLIT_TILE // ROW_CHUNK)
+    per = SPLIT_TILE // ROW_CHUNK
+    M = ntiles * per
     lst = np.empty(M, dtype=_SPLIT_DTYPE)  # (seg, c0) == p2p_split_tile_t, padded with (-1, 0)
     if _host_tables.fill_chunk_list(np.ascontiguousarray(nch, dtype=np.int64), lst) != C:
         raise RuntimeError("chunk list: size mismatch")
+    cus = CHUNK_BALANCE_CUS
+    if cus and ntiles > cus and ntiles % cus:
+        # A/B only: the chunks spread over whole CU rounds of tiles (fewer
+        # chunks per tile, the rest padding) instead of a partial last round
+        T = -(-ntiles // cus) * cus
+        q, extra = divmod(C, T)
+        cnt = np.full(T, q, dtype=np.int64)
+        cnt[:extra] += 1
+        slot = (np.arange(T, dtype=np.int64) * per)[:, None] + np.arange(per, dtype=np.int64)[None, :]
+        take = np.arange(per)[None, :] < cnt[:, None]
+        bal = np.empty(T * per, dtype=_SPLIT_DTYPE)
+        bal["seg"], bal["c0"] = -1, 0
+        bal[slot[take]] = lst[:C]
+        lst = bal
     return aligned, lst
+
+
+# A/B switch (tools/balance_ab.py): CU count to balance the chunk list over
+# whole rounds of; 0 = off (the product)
+CHUNK_BALANCE_CUS = 0
 
 
 # How a FedAvg state_dict of separately allocated tensors runs: "chunks" (the
