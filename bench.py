@@ -1743,10 +1743,21 @@ def main():
         # collective named (the process group's watchdog), well inside the
         # driver's run limit, instead of a silent hang
         tmo = datetime.timedelta(seconds=float(os.environ.get("P2P_DIST_TIMEOUT_S", "240")))
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
-        else:
-            dist.init_process_group(backend, timeout=tmo)
+        # stdout carries one JSON line: what the backends print while they
+        # connect (gloo's "[Gloo] Rank r is connected to ...", RCCL's
+        # NCCL_DEBUG lines) goes to stderr
+        sys.stdout.flush()
+        saved_fd = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
+            else:
+                dist.init_process_group(backend, timeout=tmo)
+            dist.barrier()
+        finally:
+            os.dup2(saved_fd, 1)
+            os.close(saved_fd)
         if dist.get_world_size() != world:
             raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, expected {world}")
     dev = torch.device("cuda", local)
