@@ -48,6 +48,7 @@ bytes per launch from rocprofv3 PMC FETCH_SIZE/WRITE_SIZE
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -1708,6 +1709,20 @@ def spawn_command(gpus: int, port: int, argv) -> list:
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """File descriptor 1 points at stderr inside the block (native libraries
+    printing to stdout included); Python's own stdout is flushed first."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def _free_port() -> int:
     import socket
 
@@ -1746,18 +1761,12 @@ def main():
         # stdout carries one JSON line: what the backends print while they
         # connect (gloo's "[Gloo] Rank r is connected to ...", RCCL's
         # NCCL_DEBUG lines) goes to stderr
-        sys.stdout.flush()
-        saved_fd = os.dup(1)
-        os.dup2(2, 1)
-        try:
+        with stdout_to_stderr():
             if backend == "nccl":
                 dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
             else:
                 dist.init_process_group(backend, timeout=tmo)
             dist.barrier()
-        finally:
-            os.dup2(saved_fd, 1)
-            os.close(saved_fd)
         if dist.get_world_size() != world:
             raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, expected {world}")
     dev = torch.device("cuda", local)

@@ -132,3 +132,15 @@ def test_gather_switch_parses():
         assert all(ex in sharded.EXCHANGES for _, ex in bench.GATHER_LEGS.values())
     finally:
         _sys.argv = saved
+
+
+def test_stdout_to_stderr_moves_native_prints(capfd):
+    """bench's stdout is one JSON line: what native code prints to fd 1
+    while the process group connects (gloo, RCCL debug) lands on stderr."""
+    import os as _os
+
+    with bench.stdout_to_stderr():
+        _os.write(1, b"[Gloo] Rank 0 is connected\n")
+    _os.write(1, b"{}\n")
+    out, err = capfd.readouterr()
+    assert out == "{}\n" and "[Gloo] Rank 0 is connected" in err
