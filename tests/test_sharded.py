@@ -539,3 +539,42 @@ def test_gpu_world1_nccl_allgather_path(cuda):
     want = oracle.fedavg(peers, oracle.synth(3 * 70_001, 37, 0xFFFFF, 5e-2))[0].tobytes()
     assert backend == "nccl" and b == want
     assert got["planes_p2p"] == (want, "nccl")
+
+
+def _subgroup_exchange_worker(rank, world, port, q):
+    """exchange_ over a process subgroup: group ranks map to global ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        members = [0, 2]
+        grp = dist.new_group(members)  # every rank takes part in new_group
+        got = None
+        if rank in members:
+            C, r = 5, members.index(rank)
+            mine = torch.arange(C, dtype=torch.float32) + 100 * rank
+            for kind in sharded.EXCHANGES:
+                out = torch.full((2 * C,), -1.0)
+                sharded.exchange_(out, mine, grp, kind)
+                got = (got or {}) | {kind: out.tolist()}
+            assert r == members.index(rank)
+        q.put((rank, got))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_over_a_subgroup():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_exchange_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    want = [float(i) for i in range(5)] + [200.0 + i for i in range(5)]
+    assert got[1] is None
+    for r in (0, 2):
+        assert got[r] == {"all_gather": want, "p2p": want}
