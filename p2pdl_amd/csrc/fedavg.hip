@@ -267,6 +267,38 @@ template <int AUX>
 __device__ __forceinline__ void dma16(const float* src, float* lds_dst) {
   __builtin_amdgcn_global_load_lds((P2P_GLOBAL void*)(const_cast<float*>(src)), (P2P_LDS void*)lds_dst, 16, 0, AUX);
 }
+// The split kernel's w path: the w slice DMA'd into LDS beside the stages
+// (cache policy P2P_W_DMA_AUX: 0 plain, 2 nontemporal) and the epilogue's w /
+// out stores (P2P_W_STORE_AUX: -1 plain global stores; else buffer stores
+// with those cache-policy bits -- bit 0 sc0, bit 1 nt, bit 4 sc1).  Same
+// bits either way.  The stores were the split kernel's per-tile cost: the
+// lab's queue kernel with its w stores dropped runs 4-14% faster at K = 64 /
+// 16 while dropping the w DMA alone changes ~1% (tools/split_fixed_lab.hip
+// probes, profiles/r06/wpath).  Device-scope (sc1) stores, written through
+// the XCD's L2 instead of lingering there dirty among the peer stream, with
+// the w DMA nontemporal: same process, launch by launch against plain
+// stores (tools/lib_pair_ab.py, tools/variants/wpath_*.py): K = 256 x 16.8M
+// +1.1%, 64 x 100M +2.1%, 16 x 11.7M +2.1%, 16 x 100M +3.6%, the cfg2 rows
+// kernel +1.0%, the chunk list +1.3% -- the best of nt / sc0 sc1 / sc1 nt /
+// sc0 sc1 nt.
+#ifndef P2P_W_DMA_AUX
+#define P2P_W_DMA_AUX 2
+#endif
+#ifndef P2P_W_STORE_AUX
+#define P2P_W_STORE_AUX 16
+#endif
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+// v to base[off .. off + 3]: base wave-uniform, off < kSTile (a tile's or a
+// chunk's floats past base).
+__device__ __forceinline__ void st_w(float* base, uint32_t off, f4 v) {
+#if P2P_W_STORE_AUX < 0
+  st(base + off, v);
+#else
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, kSTile * 4, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, off * 4u, 0, P2P_W_STORE_AUX);
+#endif
+}
+
 // Four ds_read_b128 of this lane's part at LDS byte address a, waited in the
 // same statement (hipcc neither counts nor reorders around it).
 __device__ __forceinline__ void lds_read4(f4 (&x)[4], uint32_t a) {
@@ -333,7 +365,7 @@ __device__ __forceinline__ void rows_tile(const p2p_row_chunk_t* ch, int K, int 
 #pragma unroll
     for (int r = 0; r < kSRpw; ++r) {
       const int idx = lane * 4 + r * 256;
-      if (idx + 4 <= valid) dma16<0>(cwp + idx, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
+      if (idx + 4 <= valid) dma16<P2P_W_DMA_AUX>(cwp + idx, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
     }
   }
   f4 acc[kSRpw];
@@ -349,7 +381,7 @@ __device__ __forceinline__ void rows_tile(const p2p_row_chunk_t* ch, int K, int 
   for (int r = 0; r < kSRpw; ++r) {
     const int idx = lane * 4 + r * 256;
     if (idx + 4 <= valid) {
-      st(cwp + idx, apply4(wq[r], lr, m[r]));  // (:36-38)
+      st_w(cwp, idx, apply4(wq[r], lr, m[r]));  // (:36-38)
     } else if (idx < valid) {  // the key's last, partial float4
       const float mv[4] = {m[r].x, m[r].y, m[r].z, m[r].w};
       for (int e = 0; idx + e < valid; ++e) stg(cwp + idx + e, apply_lr(ldg(cwp + idx + e), lr, mv[e]));
@@ -423,7 +455,7 @@ __device__ __forceinline__ void chunks_tile(const p2p_split_tile_t* list, const 
 #pragma unroll
     for (int r = 0; r < kSRpw; ++r) {
       const int idx = lane * 4 + r * 256;
-      if (idx + 4 <= valid) dma16<0>(cwp + idx, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
+      if (idx + 4 <= valid) dma16<P2P_W_DMA_AUX>(cwp + idx, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
     }
   }
   f4 acc[kSRpw];
@@ -435,7 +467,7 @@ __device__ __forceinline__ void chunks_tile(const p2p_split_tile_t* list, const 
   if (cop) {
 #pragma unroll
     for (int r = 0; r < kSRpw; ++r)
-      if (lane * 4 + r * 256 + 4 <= valid) st(cop + lane * 4 + r * 256, m[r]);
+      if (lane * 4 + r * 256 + 4 <= valid) st_w(cop, lane * 4 + r * 256, m[r]);
   }
   if (cwp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w DMA (and its older stores)
@@ -443,7 +475,7 @@ __device__ __forceinline__ void chunks_tile(const p2p_split_tile_t* list, const 
     lds_read4(wq, lds0 + static_cast<uint32_t>(kSS * kSTile * 4) + mine);
 #pragma unroll
     for (int r = 0; r < kSRpw; ++r)
-      if (lane * 4 + r * 256 + 4 <= valid) st(cwp + lane * 4 + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
+      if (lane * 4 + r * 256 + 4 <= valid) st_w(cwp, lane * 4 + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
   }
   if (valid & 3) {  // the key's last, partial float4: its lane sums it from the peers themselves
     const int idx = static_cast<int>(valid & ~int64_t(3));
@@ -461,9 +493,11 @@ template <bool RECIP, typename Hook>
 __device__ __forceinline__ void flat_tile(const SplitTile& tl, int K, int lane, float lr, float fk, float inv,
                                           float* lds, uint32_t lds0, uint32_t mine, int& slot, int cw, Hook&& hook) {
   const int64_t o = tl.c0 + cw * kSRpw * 256 + lane * 4;
+  const uint32_t oi = static_cast<uint32_t>(cw * kSRpw * 256 + lane * 4);  // o - tl.c0
   if (tl.w) {
 #pragma unroll
-    for (int r = 0; r < kSRpw; ++r) dma16<0>(tl.w + o + r * 256, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
+    for (int r = 0; r < kSRpw; ++r)
+      dma16<P2P_W_DMA_AUX>(tl.w + o + r * 256, &lds[kSS * kSTile + (cw * kSRpw + r) * 256]);
   }
   f4 acc[kSRpw];
   sum_stages(acc, K, lds0, mine, slot, hook);
@@ -471,15 +505,17 @@ __device__ __forceinline__ void flat_tile(const SplitTile& tl, int K, int lane, 
 #pragma unroll
   for (int r = 0; r < kSRpw; ++r) m[r] = div4<RECIP>(acc[r], fk, inv);  // (:31-32)
   if (tl.out) {
+    float* ob = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(tl.out + tl.c0)));
 #pragma unroll
-    for (int r = 0; r < kSRpw; ++r) st(tl.out + o + r * 256, m[r]);
+    for (int r = 0; r < kSRpw; ++r) st_w(ob, oi + r * 256, m[r]);
   }
   if (tl.w) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w DMA (and its older stores)
     f4 wq[kSRpw];
     lds_read4(wq, lds0 + static_cast<uint32_t>(kSS * kSTile * 4) + mine);
+    float* wb = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(tl.w + tl.c0)));
 #pragma unroll
-    for (int r = 0; r < kSRpw; ++r) st(tl.w + o + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
+    for (int r = 0; r < kSRpw; ++r) st_w(wb, oi + r * 256, apply4(wq[r], lr, m[r]));  // (:36-38)
   }
 }
 

@@ -29,6 +29,8 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <cstring>
+#include <string>
 #include <vector>
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
@@ -131,7 +133,13 @@ __global__ __launch_bounds__(64 * (L + C)) void split_tile_blocks(const float* c
 // issues that tile's first stage ((j+1)K - S + 1 > jK + kR for K >= 8).
 // Every wave leaves once the queue is exhausted: the same number of
 // barriers (K per tile) on both sides.
-template <int L, int C, int S, int TF>
+// The w path's parts: WD = w DMA (0 none, 1 plain, 2 nontemporal), ST = the
+// epilogue's stores (0 none, 1 plain, 2 nontemporal).  WD 0 or ST 0 is a
+// probe, not FedAvg (WD 0 applies to w = 0; ST 0 keeps the sums live by a
+// store guarded by a NaN test that never holds).
+// ST = 3: buffer stores with cache-policy bits AUX (bit 0 sc0, bit 1 nt,
+// bit 4 sc1), through a descriptor at the tile's w base.
+template <int L, int C, int S, int TF, int WD = 1, int ST = 1, int AUX = 0>
 __global__ __launch_bounds__(64 * (L + C)) void split_queue(const float* const* __restrict__ peers, int K,
                                                             long ntiles, float* w, float lr, int* counter) {
   constexpr int PER = TF / 256 / L, RPW = TF / 256 / C;
@@ -177,8 +185,13 @@ __global__ __launch_bounds__(64 * (L + C)) void split_queue(const float* const* 
     int claim = 0;
     if (cw == 0 && lane == 0) claim = atomicAdd(counter, 1);
     float* wt = w + t * TF + cw * RPW * 256 + lane * 4;
+    if (WD) {
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) dma16<0>(wt + r * 256, &lds[S * TF + (cw * RPW + r) * 256]);
+      for (int r = 0; r < RPW; ++r) {
+        if (WD == 2) dma16<2>(wt + r * 256, &lds[S * TF + (cw * RPW + r) * 256]);
+        else dma16<0>(wt + r * 256, &lds[S * TF + (cw * RPW + r) * 256]);
+      }
+    }
     f4 acc[RPW];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};
@@ -194,7 +207,36 @@ __global__ __launch_bounds__(64 * (L + C)) void split_queue(const float* const* 
       for (int r = 0; r < RPW; ++r) acc[r] += x[r];
       slot = slot + 1 == S ? 0 : slot + 1;
     }
-    epilogue<RPW>(acc, fk, lr, lds0 + (uint32_t)(S * TF * 4) + mine, wt);
+    if (ST == 0) {
+      if (WD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (acc[0].x != acc[0].x) *(GLOBAL f4*)wt = acc[0];  // never: the inputs hold no NaN
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's w DMA
+      f4 wq[RPW];
+      if (WD) {
+        lds_read_part<RPW>(wq, lds0 + (uint32_t)(S * TF * 4) + mine);
+      } else {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) wq[r] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        f4 o;
+        o.x = apply_lr(wq[r].x, lr, acc[r].x / fk); o.y = apply_lr(wq[r].y, lr, acc[r].y / fk);
+        o.z = apply_lr(wq[r].z, lr, acc[r].z / fk); o.w = apply_lr(wq[r].w, lr, acc[r].w / fk);
+        if (ST == 3) {
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc(w + t * TF, 0, TF * 4, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o), rs,
+              (cw * RPW * 256 + lane * 4 + r * 256) * 4, 0, AUX);
+        } else if (ST == 2) {
+          __builtin_nontemporal_store(o, (GLOBAL f4*)(wt + r * 256));
+        } else {
+          *(GLOBAL f4*)(wt + r * 256) = o;  // (:31-38)
+        }
+      }
+    }
     t = __builtin_amdgcn_readfirstlane((int)tq[(j + 1) & 3]);
     if (t >= ntiles) break;
   }
@@ -234,6 +276,14 @@ int main(int argc, char** argv) {
     const long tiles = n / TF; const int g = (int)std::min<long>(tiles, CUS); \
     CHECK(hipMemcpyAsync(COUNTER, &g, 4, hipMemcpyHostToDevice, 0)); \
     hipLaunchKernelGGL((split_queue<L, C, S, TF>), dim3(g), dim3(64 * (L + C)), 0, 0, p, K, tiles, w, 0.1f, COUNTER); }}
+#define QV(NAME, WD, ST) {NAME, [](const float** p, int K, long n, float* w) { \
+    const long tiles = n / 8192; const int g = (int)std::min<long>(tiles, CUS); \
+    CHECK(hipMemcpyAsync(COUNTER, &g, 4, hipMemcpyHostToDevice, 0)); \
+    hipLaunchKernelGGL((split_queue<4, 8, 3, 8192, WD, ST>), dim3(g), dim3(64 * 12), 0, 0, p, K, tiles, w, 0.1f, COUNTER); }}
+#define QB(NAME, AUX) {NAME, [](const float** p, int K, long n, float* w) { \
+    const long tiles = n / 8192; const int g = (int)std::min<long>(tiles, CUS); \
+    CHECK(hipMemcpyAsync(COUNTER, &g, 4, hipMemcpyHostToDevice, 0)); \
+    hipLaunchKernelGGL((split_queue<4, 8, 3, 8192, 2, 3, AUX>), dim3(g), dim3(64 * 12), 0, 0, p, K, tiles, w, 0.1f, COUNTER); }}
   std::vector<Var> vars = {
       TB("P  L4C8 S3 T8192 (product)", 4, 8, 3, 8192),
       TB("P4 L4C8 S4 T8192", 4, 8, 4, 8192),
@@ -241,7 +291,28 @@ int main(int argc, char** argv) {
       TB("H  L2C4 S3 T4096 (2/CU)", 2, 4, 3, 4096),
       TB("H4 L2C4 S4 T4096 (2/CU)", 2, 4, 4, 4096),
       TB("HW L4C8 S3 T4096 (2/CU)", 4, 8, 3, 4096),
+      QV("QN queue, nt stores", 1, 2),
+      QV("QNN queue, nt w DMA + nt stores", 2, 2),
+      QV("QW queue, w DMA, no stores (probe)", 1, 0),
+      QV("QS queue, stores, no w DMA (probe)", 0, 1),
+      QV("QR queue, peers only (probe)", 0, 0),
+      QB("QB0 nt w DMA, buffer store plain", 0),
+      QB("QB2 nt w DMA, buffer store nt", 2),
+      QB("QB3 nt w DMA, buffer store sc0 nt", 3),
+      QB("QB16 nt w DMA, buffer store sc1", 16),
+      QB("QB17 nt w DMA, buffer store sc0 sc1", 17),
+      QB("QB18 nt w DMA, buffer store sc1 nt", 18),
+      QB("QB19 nt w DMA, buffer store sc0 sc1 nt", 19),
   };
+  // ONLY="P Q QR" (first token of each name) limits the variants
+  if (const char* only = getenv("ONLY")) {
+    std::vector<Var> keep;
+    for (auto& v : vars) {
+      std::string tok(v.name, strcspn(v.name, " "));
+      if ((" " + std::string(only) + " ").find(" " + tok + " ") != std::string::npos) keep.push_back(v);
+    }
+    vars = keep;
+  }
   CHECK(hipMemcpy(ref, w0, 4 * n, hipMemcpyDeviceToDevice));
   vars[0].fn(dp, K, n, ref);
   CHECK(hipGetLastError());
@@ -249,6 +320,7 @@ int main(int argc, char** argv) {
   CHECK(hipMemcpy(href.data(), ref, 4 * n, hipMemcpyDeviceToHost));
   bool all_ok = true;
   for (size_t v = 1; v < vars.size(); ++v) {
+    if (strstr(vars[v].name, "(probe)")) continue;  // not FedAvg
     CHECK(hipMemcpy(w, w0, 4 * n, hipMemcpyDeviceToDevice));
     vars[v].fn(dp, K, n, w);
     CHECK(hipGetLastError());
@@ -273,7 +345,7 @@ int main(int argc, char** argv) {
   printf("K=%d n=%ld  FedAvg bytes 4n(K+2) = %.3f GB, CUs %d\n", K, n, 4.0 * n * (K + 2) / 1e9, CUS);
   for (size_t v = 0; v < vars.size(); ++v) {
     std::sort(ms[v].begin(), ms[v].end());
-    const double bytes = 4.0 * n * (K + 2);
+    const double bytes = 4.0 * n * (K + 2);  // every variant priced at FedAvg's bytes
     const float t = ms[v][ms[v].size() / 2];
     printf("%-30s median %8.4f ms  %.4f of 8 TB/s  best %.4f\n", vars[v].name, t, bytes / (t * 1e-3) / 8e12,
            bytes / (ms[v][0] * 1e-3) / 8e12);
