@@ -36,6 +36,25 @@ __device__ __forceinline__ void st4(float* p, f4 v) {
   if (NT) st4_nt(p, v); else *reinterpret_cast<f4*>(p) = v;
 }
 
+// The whole-tile stores' cache policy (P2P_DELTA_STORE_AUX): -1 nontemporal
+// global stores; else buffer stores with those cache-policy bits (bit 0
+// sc0, bit 1 nt, bit 4 sc1) through a descriptor at the tile's base -- the
+// A/B builds' knob (tools/variants/delta_*.py; the split kernel's w stores
+// won by device-scope sc1, fedavg.hip st_w).
+#ifndef P2P_DELTA_STORE_AUX
+#define P2P_DELTA_STORE_AUX 16
+#endif
+typedef uint32_t du4 __attribute__((ext_vector_type(4)));
+// v to base[off .. off + 3]: base wave-uniform, off < 2^20 floats past it.
+__device__ __forceinline__ void st4_tile(float* base, uint32_t off, f4 v) {
+#if P2P_DELTA_STORE_AUX < 0
+  st4_nt(base + off, v);
+#else
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 1u << 22, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(du4, v), rs, off * 4u, 0, P2P_DELTA_STORE_AUX);
+#endif
+}
+
 // One tile of kBlock*4*NV floats (the segments kernel and the ABI's
 // P2P_DELTA_TILE use NV = kDNV).
 template <int NV = kDNV, bool NT = true>
@@ -53,6 +72,17 @@ __device__ __forceinline__ void delta_tile(const float* cur, float* prev, float*
     if (!first) {
 #pragma unroll
       for (int v = 0; v < NV; ++v) p[v] = ld4_nt(prev + base + kBlock * 4 * v);
+    }
+    if (NT) {  // descriptors at the tile's base (wave-uniform): the store policy above
+      float* db = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(delta + tile0)));
+      float* pb = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(prev + tile0)));
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const uint32_t o = static_cast<uint32_t>(4 * threadIdx.x + kBlock * 4 * v);
+        st4_tile(db, o, first ? c[v] : c[v] - p[v]);  // (:279) or the first-round copy (:275)
+        st4_tile(pb, o, c[v]);                          // clone (:282)
+      }
+      return;
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {

@@ -224,8 +224,23 @@ __device__ __forceinline__ void robust_one(const float* const* peers, int K, int
   const int64_t i = c0 + tid_x();
   if (i >= n) return;
   const float agg = robust_coord<KP, RULE, MODE, PAD>(peers, K, trim_b, c0, tid_x() * 4u);
+#if P2P_ROBUST_STORE_AUX < 0
   if (out) stg(out + i, agg);
   if (w) stg(w + i, apply_lr(ldg(w + i), lr, agg));
+#else
+  // descriptors at the tile's base (wave-uniform), the lane's float at tid * 4
+  if (out) {
+    float* ob = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(out + c0)));
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(agg), __builtin_amdgcn_make_buffer_rsrc(ob, 0, kRobustTile * 4, 0x00020000),
+                                          tid_x() * 4u, 0, P2P_ROBUST_STORE_AUX);
+  }
+  if (w) {
+    float* wb = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(w + c0)));
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(apply_lr(ldg(w + i), lr, agg)),
+                                          __builtin_amdgcn_make_buffer_rsrc(wb, 0, kRobustTile * 4, 0x00020000),
+                                          tid_x() * 4u, 0, P2P_ROBUST_STORE_AUX);
+  }
+#endif
 }
 
 // 2-D grid (p2p_common.h tile_grid): tile t = blockIdx.y * gx + blockIdx.x.

@@ -5,6 +5,14 @@
 #pragma once
 #include "p2p_common.h"
 
+// The robust kernels' w / out stores: -1 plain (global stores, or buffer
+// stores without cache-policy bits); else buffer stores with these bits (bit
+// 0 sc0, bit 1 nt, bit 4 sc1) -- the A/B builds' knob (the FedAvg split
+// kernel's and the delta's stores won by device-scope sc1).
+#ifndef P2P_ROBUST_STORE_AUX
+#define P2P_ROBUST_STORE_AUX 18
+#endif
+
 namespace p2p {
 
 // NaN-free fast path: the networks run on the float values themselves.

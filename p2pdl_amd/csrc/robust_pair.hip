@@ -467,11 +467,12 @@ __device__ __forceinline__ void pair_tile(const float* const* __restrict__ peers
   }
   if (h == 0 && live) {  // wave 0 holds the aggregate
     if constexpr (NARROW) {  // a live lane's offset is its coordinate's
-      if (O) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(agg), flat_rsrc(O), lane_off, 0, 0);
+      constexpr int kSt = P2P_ROBUST_STORE_AUX < 0 ? 0 : P2P_ROBUST_STORE_AUX;
+      if (O) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(agg), flat_rsrc(O), lane_off, 0, kSt);
       if (W) {
         const auto r = flat_rsrc(W);
         const float wv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, lane_off, 0, 0));
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(apply_lr(wv, lr, agg)), r, lane_off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(apply_lr(wv, lr, agg)), r, lane_off, 0, kSt);
       }
     } else {
       if (O) stg(O + i, agg);

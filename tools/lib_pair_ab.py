@@ -13,7 +13,8 @@ chunk list (p2p_fedavg_split_chunks_f32, tables built once by the product).
 Measurement tool, not product.
 and ("rows:K:scale") the same model landed in a DeviceInbox slab (the rows
 kernel).
-usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n | sd:K:scale | rows:K:scale> ...
+and ("delta:n") the trainer delta over n parameters.
+usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n[:median|trimmed] | sd:K:scale | rows:K:scale | delta:n> ...
   tag "prod" = p2pdl_amd/libp2pdl_hip.so, tag X = tools/libp2pdl_X.so"""
 import ctypes
 import os
@@ -43,7 +44,44 @@ def load(tag):
     r.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_float,
                   ctypes.c_void_p]
     r.restype = ctypes.c_int32
-    return f, c, r
+    d = lib.p2p_delta_snapshot_f32
+    d.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
+    d.restype = ctypes.c_int32
+    return f, c, r, d
+
+
+def delta_case(fns, tags, n, reps, dev):
+    """The trainer delta (p2p_delta_snapshot_f32) over n parameters: each
+    build from the same cur / prev, outputs bit-compared, then timed launch by
+    launch (16 B per parameter: read cur and prev, write delta and prev)."""
+    cur = torch.empty(n, dtype=torch.float32, device=dev)
+    prev0 = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.fill_synthetic_(cur, 0x5EED0003, 1, 1e-1)
+    ops.fill_synthetic_(prev0, 0x5EED0003, 2, 1e-1)
+    prev, delta = prev0.clone(), torch.empty_like(cur)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    outs = {}
+    for t in tags:
+        prev.copy_(prev0)
+        assert fns[t][3](cur.data_ptr(), prev.data_ptr(), delta.data_ptr(), n, 0, st) == 0
+        torch.cuda.synchronize()
+        outs[t] = (delta.cpu().numpy().view(np.uint32), prev.cpu().numpy().view(np.uint32))
+    same = all(np.array_equal(outs[t][0], outs[tags[0]][0]) and np.array_equal(outs[t][1], outs[tags[0]][1])
+               for t in tags)
+    ms = {t: [] for t in tags}
+    for r in range(reps):
+        for t in (tags if r % 2 == 0 else tags[::-1]):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(2_000_000)
+            e0.record()
+            fns[t][3](cur.data_ptr(), prev.data_ptr(), delta.data_ptr(), n, 0, st)
+            e1.record()
+            torch.cuda.synchronize()
+            ms[t].append(e0.elapsed_time(e1))
+    report("delta (16 B per parameter)", 2, n, same, ms)  # 4 n (K + 2) with K = 2: 16 B per parameter
+    del cur, prev0, prev, delta
+    torch.cuda.empty_cache()
+    return same
 
 
 def rows_case(fns, tags, K, scale, reps, dev):
@@ -161,11 +199,16 @@ def main():
     fns = {t: load(t) for t in tags}
     ok = True
     for case in cases:
+        if case[0] == "delta":
+            ok &= delta_case(fns, tags, int(case[1]), reps, dev)
+            continue
         if case[0] in ("sd", "rows"):
             fn = state_dict_case if case[0] == "sd" else rows_case
             ok &= fn(fns, tags, int(case[1]), int(case[2]), reps, dev)
             continue
         K, n = int(case[0]), int(case[1])
+        rule = {"fedavg": 0, "median": 1, "trimmed": 2}[case[2] if len(case) > 2 else "fedavg"]
+        tb = ops.trim_count(K, 0.2) if rule == 2 else 0
         pitch = -(-n // 64) * 64
         slab = torch.empty((K, pitch), dtype=torch.float32, device=dev)
         for p in range(K):
@@ -177,7 +220,7 @@ def main():
         st = torch.cuda.current_stream(dev).cuda_stream
         for t, f in fns.items():
             w = w0.clone()
-            assert f[0](table.data_ptr(), K, n, 0, 0, 0.1, w.data_ptr(), None, st) == 0
+            assert f[0](table.data_ptr(), K, n, rule, tb, 0.1, w.data_ptr(), None, st) == 0
             torch.cuda.synchronize()
             outs[t] = w.cpu().numpy().view(np.uint32)
         same = all(np.array_equal(outs[t], outs[tags[0]]) for t in tags)
@@ -190,11 +233,11 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 torch.cuda._sleep(2_000_000)
                 e0.record()
-                fns[t][0](table.data_ptr(), K, n, 0, 0, 0.1, w.data_ptr(), None, st)
+                fns[t][0](table.data_ptr(), K, n, rule, tb, 0.1, w.data_ptr(), None, st)
                 e1.record()
                 torch.cuda.synchronize()
                 ms[t].append(e0.elapsed_time(e1))
-        report(f"flat K={K}", K, n, same, ms)
+        report(f"flat K={K}" + (f" {case[2]}" if len(case) > 2 else ""), K, n, same, ms)
         del slab, table, w0, w
         torch.cuda.empty_cache()
     return 0 if ok else 1

@@ -1,0 +1,8 @@
+"""A/B variant (round 6): the robust kernels' w / out stores as buffer
+stores with cache-policy bits 16 (bit 0 sc0, bit 1 nt, bit 4 sc1); see
+robust_nets.h P2P_ROBUST_STORE_AUX."""
+p = "robust_nets.h"
+s = open(p).read()
+old = "#define P2P_ROBUST_STORE_AUX -1\n"
+assert old in s
+open(p, "w").write(s.replace(old, "#define P2P_ROBUST_STORE_AUX 16\n"))
