@@ -117,17 +117,17 @@ __global__ __launch_bounds__(kBlock) void delta_segments_kernel(const p2p_delta_
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    const int64_t tb = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&segs[mid].tile_begin))));
+    const int64_t tb = ldc(&segs[mid].tile_begin);
     if (tb <= t) lo = mid; else hi = mid - 1;
     lo = __builtin_amdgcn_readfirstlane(lo);
     hi = __builtin_amdgcn_readfirstlane(hi);
   }
   const p2p_delta_segment_t* sp = segs + lo;
-  const float* cur = reinterpret_cast<const float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->cur))));
-  float* prev = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->prev))));
-  float* delta = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->delta))));
-  const int64_t n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
-  const int64_t tb = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->tile_begin))));
+  const float* cur = ldc(&sp->cur);
+  float* prev = ldc(&sp->prev);
+  float* delta = ldc(&sp->delta);
+  const int64_t n = ldc(&sp->n);
+  const int64_t tb = ldc(&sp->tile_begin);
   delta_tile<kDNV, true>(cur, prev, delta, n, (t - tb) * kDTile, first != 0);
 }
 

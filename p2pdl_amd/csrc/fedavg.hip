@@ -322,12 +322,10 @@ template <bool SEGS>
 __device__ __forceinline__ SplitTile split_tile(const float* const* peers, float* w, float* out,
                                                 const p2p_split_tile_t* tiles, const Seg* segs, int64_t t) {
   if constexpr (SEGS) {
-    const int64_t seg = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&tiles[t].seg))));
-    const int64_t c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&tiles[t].c0))));
+    const int64_t seg = ldc(&tiles[t].seg);
+    const int64_t c0 = ldc(&tiles[t].c0);
     const Seg* sp = segs + seg;
-    return SplitTile{reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->peers)))),
-                     reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->w)))),
-                     reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->out)))), c0};
+    return SplitTile{ldc(&sp->peers), ldc(&sp->w), ldc(&sp->out), c0};
   } else {
     return SplitTile{peers, w, out, t * kSTile};
   }
@@ -359,8 +357,8 @@ __device__ __forceinline__ void sum_stages(f4 (&acc)[kSRpw], int K, uint32_t lds
 template <bool RECIP, typename Hook>
 __device__ __forceinline__ void rows_tile(const p2p_row_chunk_t* ch, int K, int lane, float lr, float fk, float inv,
                                           float* lds, uint32_t lds0, uint32_t mine, int& slot, int cw, Hook&& hook) {
-  float* cwp = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&ch->w))));
-  const int64_t valid = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&ch->valid))));
+  float* cwp = ldc(&ch->w);
+  const int64_t valid = ldc(&ch->valid);
   if (cwp) {
 #pragma unroll
     for (int r = 0; r < kSRpw; ++r) {
@@ -408,14 +406,13 @@ struct ChunkSrc {
   uint32_t bytes;             // the DMA range: the chunk's whole float4s, in bytes
 };
 __device__ __forceinline__ ChunkSrc chunk_src(const p2p_split_tile_t* list, const Seg* segs, int64_t c) {
-  const int64_t seg = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&list[c].seg))));
+  const int64_t seg = ldc(&list[c].seg);
   if (seg < 0) return ChunkSrc{nullptr, 0, 0u};
-  const int64_t c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&list[c].c0))));
+  const int64_t c0 = ldc(&list[c].c0);
   const Seg* sp = segs + seg;
-  const int64_t n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
+  const int64_t n = ldc(&sp->n);
   const int64_t valid = n - c0 < P2P_ROW_CHUNK ? n - c0 : P2P_ROW_CHUNK;
-  return ChunkSrc{reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->peers)))), c0,
-                  static_cast<uint32_t>((valid & ~int64_t(3)) * 4)};
+  return ChunkSrc{ldc(&sp->peers), c0, static_cast<uint32_t>((valid & ~int64_t(3)) * 4)};
 }
 constexpr int kChunkDma = P2P_ROW_CHUNK / 256;  // 1-KiB DMAs per chunk per stage
 static_assert(kSPer == 2 * kChunkDma, "a loader wave streams two chunks per stage");
@@ -436,18 +433,18 @@ template <bool RECIP, typename Hook>
 __device__ __forceinline__ void chunks_tile(const p2p_split_tile_t* list, const Seg* segs, int64_t c, int K, int lane,
                                             float lr, float fk, float inv, float* lds, uint32_t lds0, uint32_t mine,
                                             int& slot, int cw, Hook&& hook) {
-  const int64_t seg = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&list[c].seg))));
+  const int64_t seg = ldc(&list[c].seg);
   const float* const* cp = nullptr;
   float *cwp = nullptr, *cop = nullptr;
   int64_t c0 = 0, valid = 0;
   if (seg >= 0) {
     const Seg* sp = segs + seg;
-    c0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&list[c].c0))));
-    const int64_t n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
+    c0 = ldc(&list[c].c0);
+    const int64_t n = ldc(&sp->n);
     valid = n - c0 < P2P_ROW_CHUNK ? n - c0 : P2P_ROW_CHUNK;
-    cp = reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->peers))));
-    float* wb = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->w))));
-    float* ob = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->out))));
+    cp = ldc(&sp->peers);
+    float* wb = ldc(&sp->w);
+    float* ob = ldc(&sp->out);
     cwp = wb ? wb + c0 : nullptr;
     cop = ob ? ob + c0 : nullptr;
   }

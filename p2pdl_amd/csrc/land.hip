@@ -27,17 +27,17 @@ __device__ __forceinline__ p2p_land_segment_t load_land_segment(const p2p_land_s
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    const int64_t tb = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&segs[mid].tile_begin))));
+    const int64_t tb = ldc(&segs[mid].tile_begin);
     if (tb <= t) lo = mid; else hi = mid - 1;
     lo = __builtin_amdgcn_readfirstlane(lo);
     hi = __builtin_amdgcn_readfirstlane(hi);
   }
   const p2p_land_segment_t* sp = segs + lo;
   p2p_land_segment_t s;
-  s.src_off = uniform_u64(ldg(&sp->src_off));
-  s.dst = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->dst))));
-  s.n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
-  s.tile_begin = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->tile_begin))));
+  s.src_off = ldc(&sp->src_off);
+  s.dst = ldc(&sp->dst);
+  s.n = ldc(&sp->n);
+  s.tile_begin = ldc(&sp->tile_begin);
   return s;
 }
 

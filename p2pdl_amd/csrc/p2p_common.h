@@ -55,6 +55,15 @@ template <typename T>
 __device__ __forceinline__ T* table_at(T* const* table, int k) {
   return reinterpret_cast<T*>(((const P2P_CONST uint64_t*)(table))[k]);
 }
+// A wave-uniform field of a host-built, launch-read-only table (tile lists,
+// chunk lists, segment descriptors) as a scalar s_load.  Read through GLOBAL
+// (ldg) it is a vector load + readfirstlane, and hipcc waits for it with
+// s_waitcnt vmcnt(0): in a loader wave that drains the whole LDS-DMA ring,
+// in a consumer wave it waits out the previous tile's stores.
+template <typename T>
+__device__ __forceinline__ T ldc(const T* p) {
+  return *(const P2P_CONST T*)(p);
+}
 
 // Work-item / work-group ids as intrinsics (the grid size is a kernel
 // argument where a loop strides by it).  The robust
@@ -79,18 +88,18 @@ __device__ __forceinline__ Seg load_segment(const Seg* segs, int nseg, int64_t t
   int lo = 0, hi = nseg - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    const int64_t tb = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&segs[mid].tile_begin))));
+    const int64_t tb = ldc(&segs[mid].tile_begin);
     if (tb <= t) lo = mid; else hi = mid - 1;
     lo = __builtin_amdgcn_readfirstlane(lo);
     hi = __builtin_amdgcn_readfirstlane(hi);
   }
   const Seg* sp = segs + lo;
   Seg s;
-  s.peers = reinterpret_cast<const float* const*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->peers))));
-  s.w = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->w))));
-  s.out = reinterpret_cast<float*>(uniform_u64(reinterpret_cast<uint64_t>(ldg(&sp->out))));
-  s.n = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->n))));
-  s.tile_begin = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(ldg(&sp->tile_begin))));
+  s.peers = ldc(&sp->peers);
+  s.w = ldc(&sp->w);
+  s.out = ldc(&sp->out);
+  s.n = ldc(&sp->n);
+  s.tile_begin = ldc(&sp->tile_begin);
   return s;
 }
 

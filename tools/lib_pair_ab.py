@@ -14,7 +14,7 @@ Measurement tool, not product.
 and ("rows:K:scale") the same model landed in a DeviceInbox slab (the rows
 kernel).
 and ("delta:n") the trainer delta over n parameters.
-usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n[:median|trimmed] | sd:K:scale | rows:K:scale | delta:n> ...
+usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n[:median|trimmed] | sd:K:scale[:place] | rows:K:scale | delta:n> ...
   tag "prod" = p2pdl_amd/libp2pdl_hip.so, tag X = tools/libp2pdl_X.so"""
 import ctypes
 import os
@@ -131,15 +131,29 @@ def rows_case(fns, tags, K, scale, reps, dev):
     return same
 
 
-def state_dict_case(fns, tags, K, scale, reps, dev):
+def state_dict_case(fns, tags, K, scale, reps, dev, place="alloc"):
     """ResNet-18's 62 shapes x scale as separately allocated tensors x K: the
     chunk list and segment table built once by the product's host code
     (ops.aggregate_ptr_table_, the model tensors `ws` it points at kept),
-    then every build's chunk kernel over the same tables."""
+    then every build's chunk kernel over the same tables.  `place`: "alloc"
+    one allocation per tensor; "packedA" the K x L tensors packed peer-major
+    in one buffer, each rounded up to A bytes (A = 512: how the caching
+    allocator carves a large freed block); "offB" one allocation per tensor,
+    the view starting B bytes in."""
     import bench
 
     sizes = [int(np.prod(sh)) for _, sh in bench.resnet18_param_shapes()] * scale
-    peers = [[torch.empty(m, dtype=torch.float32, device=dev) for m in sizes] for _ in range(K)]
+    if place.startswith("packed"):
+        a = int(place[6:]) // 4
+        rs = [-(-m // a) * a for m in sizes]
+        buf = torch.empty(K * sum(rs), dtype=torch.float32, device=dev)
+        offs = np.concatenate([[0], np.cumsum(rs)[:-1]]).astype(np.int64)
+        peers = [[buf[p * sum(rs) + int(o):p * sum(rs) + int(o) + m] for o, m in zip(offs, sizes)] for p in range(K)]
+    elif place.startswith("off"):
+        b = int(place[3:]) // 4
+        peers = [[torch.empty(m + b, dtype=torch.float32, device=dev)[b:] for m in sizes] for _ in range(K)]
+    else:
+        peers = [[torch.empty(m, dtype=torch.float32, device=dev) for m in sizes] for _ in range(K)]
     for p in range(K):
         for l, t in enumerate(peers[p]):
             ops.fill_synthetic_(t, 0x5EED0001 + l, p, 1e-2)
@@ -173,7 +187,7 @@ def state_dict_case(fns, tags, K, scale, reps, dev):
             e1.record()
             torch.cuda.synchronize()
             ms[t].append(e0.elapsed_time(e1))
-    report(f"state_dict K={K} x{scale} ({len(sizes)} separately allocated tensors, chunk list)", K, sum(sizes), same, ms)
+    report(f"state_dict K={K} x{scale} ({len(sizes)} tensors, {place}, chunk list)", K, sum(sizes), same, ms)
     del peers, ws, w0
     ops._TABLES.clear()
     torch.cuda.empty_cache()
@@ -204,7 +218,7 @@ def main():
             continue
         if case[0] in ("sd", "rows"):
             fn = state_dict_case if case[0] == "sd" else rows_case
-            ok &= fn(fns, tags, int(case[1]), int(case[2]), reps, dev)
+            ok &= fn(fns, tags, int(case[1]), int(case[2]), reps, dev, *case[3:])
             continue
         K, n = int(case[0]), int(case[1])
         rule = {"fedavg": 0, "median": 1, "trimmed": 2}[case[2] if len(case) > 2 else "fedavg"]
