@@ -6,7 +6,9 @@ tensors (ResNet-18 x 64), ops._TABLES cleared before each call, cProfile
 over the calls.  Measurement tool, not product.
 With "cached" the table is kept (the steady state of a round whose updates
 sit at the same addresses: the per-call host cost alone).
-usage: python tools/prof_general.py [calls] [mlp] [cached]"""
+With "synced" the profiled calls are synchronised one by one (the host's
+own cost per call, no backpressure from queued launches).
+usage: python tools/prof_general.py [calls] [mlp] [cached] [synced]"""
 import cProfile
 import io
 import os
@@ -65,14 +67,17 @@ def main():
         call()
     torch.cuda.synchronize()
     print(f"back to back: {(time.perf_counter() - t0) / calls * 1e6:.1f} us per call (host wall, one sync at the end)")
+    synced = "synced" in sys.argv[2:]  # a sync after every call: no queue backpressure in the host's figures
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(calls):
         call()
+        if synced:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     pr.disable()
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(40)
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(60)
     print(s.getvalue())
 
 
