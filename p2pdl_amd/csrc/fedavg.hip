@@ -746,12 +746,18 @@ static int64_t split_tiles_for(int K, int64_t full, bool all = false) {
 static dim3 split_grid(int64_t tiles) { return dim3(static_cast<unsigned>(tiles)); }
 
 // QUEUE launches (see fedavg_split_kernel): launch i takes counter pair
-// i mod kQueueSlots of g_tile_queue (zero at module load; each launch leaves
-// its pair zeroed when its last block ends).  Nothing is allocated and no
-// per-stream state kept, so the call stays graph-capturable (a captured
-// launch keeps its pair: its replays on one stream run in order).  A pair is
-// reused kQueueSlots launches later: the bound is that many split launches
-// in flight at once on one device.
+// i mod (kQueueSlots - kQueueCaptured) of g_tile_queue (zero at module load;
+// each launch leaves its pair zeroed when its last block ends).  Nothing is
+// allocated and no per-stream state kept, so the call stays graph-capturable.
+// A pair is reused kQueueSlots - kQueueCaptured launches later: the bound is
+// that many split launches in flight at once on one device.  A launch
+// captured into a graph keeps its pair for every replay, so it takes one of
+// the last kQueueCaptured pairs, never handed out again (its replays run in
+// order: a graph exec does not run concurrently with itself); were it to
+// take a rotating pair, an ordinary launch on another stream would share it
+// every 3,072 launches and, overlapping a replay, both would claim tiles from
+// one counter -- each skipping the other's.  Captures past kQueueCaptured
+// launch one block per tile (same results).
 // Which launches take the queue: 8 <= K <= kQueueMaxK, every mode.  Same
 // process, the builds alternated launch by launch on the same buffers
 // (tools/lib_pair_ab.py, profiles/r06/pair_ab), against one block per tile:
@@ -776,7 +782,19 @@ template <int MODE>
 static bool use_queue(bool share, const int32_t* k_dev, int K) {
   return queue_mode<MODE>() && !share && !k_dev && K >= kQueueMinK && K <= kQueueMaxK;
 }
+constexpr int kQueueCaptured = 1024;
 static std::atomic<uint32_t> g_queue_next{0};
+static std::atomic<uint32_t> g_queue_captured{0};
+// The counter pair of a queued launch on `st`, or -1: launch without the queue.
+static int queue_slot(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+    const uint32_t c = g_queue_captured.fetch_add(1, std::memory_order_relaxed);
+    return c < static_cast<uint32_t>(kQueueCaptured) ? kQueueSlots - kQueueCaptured + static_cast<int>(c) : -1;
+  }
+  return static_cast<int>(g_queue_next.fetch_add(1, std::memory_order_relaxed) %
+                          static_cast<uint32_t>(kQueueSlots - kQueueCaptured));
+}
 // The split kernel over ntiles tiles in mode MODE: the tile queue's
 // persistent grid of min(tiles, CUs) blocks when built with it (K from the
 // kernarg, K >= kQueueMinK), else one block per tile.  `share`
@@ -790,8 +808,8 @@ static void launch_split(const float* const* peers, int K, const int32_t* k_dev,
                          float* out, float lr, const p2p_split_tile_t* tiles, const Seg* segs,
                          const p2p_row_chunk_t* chunks, bool recip, hipStream_t st, bool share = false) {
   const dim3 block(64 * (kSL + kSC));
-  if (use_queue<MODE>(share, k_dev, K)) {
-    const int q = static_cast<int>(g_queue_next.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
+  const int q = use_queue<MODE>(share, k_dev, K) ? queue_slot(st) : -1;
+  if (q >= 0) {
     const dim3 grid(static_cast<unsigned>(ntiles < device_cus() ? ntiles : device_cus()));
     if (recip)
       hipLaunchKernelGGL((fedavg_split_kernel<true, MODE, true>), grid, block, 0, st, peers, K, k_dev, ntiles, w, out,

@@ -144,3 +144,58 @@ def test_split_kernel_graph_replay(cuda, route):
     torch.cuda.synchronize()
     for w, a in zip(ws, want):
         assert np.array_equal(w.cpu().numpy().view(np.uint32), a.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_captured_split_launch_keeps_its_queue_pair(cuda):
+    """A captured split launch owns its tile-queue counter pair (fedavg.hip
+    queue_slot): its replays on one stream, overlapping 4,200 ordinary split
+    launches on another -- more than the rotating pairs, so each of those
+    pairs is reused -- never share a counter with them.  Every output is
+    poisoned before its launch and compared on the device after it: a launch
+    that lost tiles to another's claims would leave NaNs behind.  FedAvg
+    mean (reference aggregator/aggregation.py:25-32), K = 16 over 300 whole
+    split tiles (> one per CU: the persistent grid claims tiles)."""
+    from p2pdl_amd import ops
+
+    k, n, iters = 16, 300 * 8192, 4200
+    peers = [oracle.synth(n, 83, p, 1e-2) for p in range(k)]
+    _, mean = oracle.fedavg(peers)
+    pd = [_dev(p, cuda) for p in peers]  # kept alive: the table holds only their addresses
+    table = ops.pointer_table(pd, cuda)
+    want = _dev(mean, cuda).view(torch.int32)
+    sa, sb = torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)
+    out_a = torch.empty(n, dtype=torch.float32, device=cuda)
+    out_b = torch.empty_like(out_a)
+    ops.aggregate(None, "fedavg", out=out_a, table=table)  # warm-up
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    sa.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(sa):
+        with torch.cuda.graph(g, stream=sa):
+            ops.aggregate(None, "fedavg", out=out_a, table=table)
+    torch.cuda.synchronize()
+    bad_a = torch.zeros((), dtype=torch.int64, device=cuda)
+    bad_b = torch.zeros_like(bad_a)
+    main = torch.cuda.current_stream(cuda)
+    for i in range(iters):
+        if i % 600 == 0:  # progress (and a bounded queue) for the run's hang guard
+            torch.cuda.synchronize()
+            print(f"captured-pair test: {i} / {iters}", flush=True)
+        # fork / join: both launches of an iteration start together, so the
+        # one that would share a pair overlaps the replay
+        sa.wait_stream(main)
+        sb.wait_stream(main)
+        with torch.cuda.stream(sa):
+            out_a.fill_(float("nan"))
+            g.replay()
+            bad_a += (out_a.view(torch.int32) != want).sum()
+        with torch.cuda.stream(sb):
+            out_b.fill_(float("nan"))
+            ops.aggregate(None, "fedavg", out=out_b, table=table)
+            bad_b += (out_b.view(torch.int32) != want).sum()
+        main.wait_stream(sa)
+        main.wait_stream(sb)
+    torch.cuda.synchronize()
+    assert int(bad_a) == 0 and int(bad_b) == 0, (int(bad_a), int(bad_b))
+    del pd
