@@ -6,6 +6,9 @@
 // not product.  Build:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/delta_dma_lab tools/delta_dma_lab.hip
 // Run: tools/delta_dma_lab [n floats = 268435456] [reps = 9]
+// Round 6 (last session): every layout also with device-scope (sc1) buffer
+// stores, the product's store policy since round 6 (delta.hip st4_tile), to
+// ask again whether the DMA scheme loses once the stores stop costing extra.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -19,14 +22,28 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 #define GLOBAL __attribute__((address_space(1)))
 
 __device__ __forceinline__ void st_nt(float* p, f4 v) { __builtin_nontemporal_store(v, (GLOBAL f4*)p); }
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+// ST < 0: nontemporal global store of v to base + off; else a buffer store
+// with cache-policy bits ST (16 = sc1) over a wave-uniform base.
+template <int ST>
+__device__ __forceinline__ void st_pol(float* base, uint32_t off, f4 v) {
+  if constexpr (ST < 0) {
+    st_nt(base + off, v);
+  } else {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFF0, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, off * 4u, 0, ST);
+  }
+}
 
+template <int ST>
 __global__ __launch_bounds__(256) void delta_vgpr(const float* cur, float* prev, float* delta, long n) {
-  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i + 4 > n) return;
+  const long b0 = (long)blockIdx.x * 1024;
+  const long i = b0 + threadIdx.x * 4;
+  if (b0 + 1024 > n) return;
   const f4 c = __builtin_nontemporal_load((const GLOBAL f4*)(cur + i));
   const f4 p = __builtin_nontemporal_load((const GLOBAL f4*)(prev + i));
-  st_nt(delta + i, c - p);
-  st_nt(prev + i, c);
+  st_pol<ST>(delta + b0, threadIdx.x * 4, c - p);
+  st_pol<ST>(prev + b0, threadIdx.x * 4, c);
 }
 
 template <int AUX>
@@ -48,7 +65,7 @@ __device__ __forceinline__ void lds_read_part(f4 (&x)[RPW], uint32_t a) {
 }
 
 // stage 2t = cur of tile t, stage 2t+1 = prev of tile t (per block, tiles b, b+G, ...)
-template <int L, int C, int S, int TF>
+template <int L, int C, int S, int TF, int ST>
 __global__ __launch_bounds__(64 * (L + C)) void delta_split(const float* cur, float* prev, float* delta, long ntiles) {
   constexpr int PER = TF / 256 / L, RPW = TF / 256 / C;
   static_assert((S - 2) * PER <= 63, "vmcnt");
@@ -88,11 +105,11 @@ __global__ __launch_bounds__(64 * (L + C)) void delta_split(const float* cur, fl
     __builtin_amdgcn_s_barrier();
     lds_read_part<RPW>(p, lds0 + (uint32_t)slot * (TF * 4) + mine);
     slot = slot + 1 == S ? 0 : slot + 1;
-    const long o = t * (long)TF + cw * RPW * 256 + lane * 4;
+    const uint32_t o = (uint32_t)(cw * RPW * 256 + lane * 4);
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
-      st_nt(delta + o + r * 256, c[r] - p[r]);
-      st_nt(prev + o + r * 256, c[r]);
+      st_pol<ST>(delta + t * (long)TF, o + r * 256, c[r] - p[r]);
+      st_pol<ST>(prev + t * (long)TF, o + r * 256, c[r]);
     }
   }
 }
@@ -118,16 +135,20 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&delta, 4 * n)); CHECK(hipMalloc(&ref_d, 4 * n)); CHECK(hipMalloc(&ref_p, 4 * n));
   hipLaunchKernelGGL(init, dim3(8192), dim3(256), 0, 0, cur, n, 1u);
   hipLaunchKernelGGL(init, dim3(8192), dim3(256), 0, 0, prev0, n, 2u);
-#define SP(NAME, L, C, S, TF, BPC) {NAME, [](const float* c, float* p, float* d, long n) { \
-    hipLaunchKernelGGL((delta_split<L, C, S, TF>), dim3(CUS * BPC), dim3(64 * (L + C)), 0, 0, c, p, d, n / TF); }}
+#define SP(NAME, L, C, S, TF, BPC, ST) {NAME, [](const float* c, float* p, float* d, long n) { \
+    hipLaunchKernelGGL((delta_split<L, C, S, TF, ST>), dim3(CUS * BPC), dim3(64 * (L + C)), 0, 0, c, p, d, n / TF); }}
+#define VG(NAME, ST) {NAME, [](const float* c, float* p, float* d, long n) { \
+    hipLaunchKernelGGL(delta_vgpr<ST>, dim3(n / 1024), dim3(256), 0, 0, c, p, d, n); }}
   std::vector<Var> vars = {
-      {"vgpr 1 float4/lane (product)", [](const float* c, float* p, float* d, long n) {
-         hipLaunchKernelGGL(delta_vgpr, dim3(n / 1024), dim3(256), 0, 0, c, p, d, n); }},
-      SP("split L4 C8 S4 T8192", 4, 8, 4, 8192, 1),
-      SP("split L4 C8 S4 T8192 g2", 4, 8, 4, 8192, 2),
-      SP("split L4 C8 S6 T4096", 4, 8, 6, 4096, 1),
-      SP("split L4 C8 S6 T4096 g2", 4, 8, 6, 4096, 2),
-      SP("split L2 C4 S4 T4096 g4", 2, 4, 4, 4096, 4),
+      VG("vgpr 1 float4/lane nt (r5)", -1),
+      VG("vgpr 1 float4/lane sc1 (product)", 16),
+      SP("split L4 C8 S4 T8192 nt", 4, 8, 4, 8192, 1, -1),
+      SP("split L4 C8 S4 T8192 sc1", 4, 8, 4, 8192, 1, 16),
+      SP("split L4 C8 S4 T8192 g2 sc1", 4, 8, 4, 8192, 2, 16),
+      SP("split L4 C8 S6 T4096 sc1", 4, 8, 6, 4096, 1, 16),
+      SP("split L4 C8 S6 T4096 g2 sc1", 4, 8, 6, 4096, 2, 16),
+      SP("split L2 C4 S4 T4096 g4 sc1", 2, 4, 4, 4096, 4, 16),
+      SP("split L4 C8 S4 T8192 sc1nt", 4, 8, 4, 8192, 1, 18),
   };
   // reference result (product layout), then every variant bit-compared
   CHECK(hipMemcpy(ref_p, prev0, 4 * n, hipMemcpyDeviceToDevice));
