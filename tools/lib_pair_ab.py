@@ -14,7 +14,7 @@ Measurement tool, not product.
 and ("rows:K:scale") the same model landed in a DeviceInbox slab (the rows
 kernel).
 and ("delta:n") the trainer delta over n parameters.
-usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n[:median|trimmed] | sd:K:scale[:place] | rows:K:scale | delta:n> ...
+usage: python tools/lib_pair_ab.py <reps> <tag> [<tag> ...] -- <K:n[:median|trimmed] | sd:K:scale[:place] | rows:K:scale | rowsclone:K:scale[:carve] | delta:n> ...
   tag "prod" = p2pdl_amd/libp2pdl_hip.so, tag X = tools/libp2pdl_X.so"""
 import ctypes
 import os
@@ -131,6 +131,66 @@ def rows_case(fns, tags, K, scale, reps, dev):
     return same
 
 
+def rows_vs_clones_case(fns, tags, K, scale, reps, dev, carve=""):
+    """The bench's cfg2_dropin setup in one process (round 6): a DeviceInbox
+    slab, then plain dicts of .clone()d slab-row slices (bench.py: the
+    general path's pickle.loads stand-ins), and three launches alternated rep
+    by rep with the first build: the rows kernel over the slab, the chunk list
+    over the clones, the chunk list over the slab rows' own views.  "carve":
+    a 16 GB block allocated and freed first, so the clones are carved from
+    the caching allocator's cached block as after bench's cfg3 planes."""
+    import bench
+    from p2pdl_amd.node.inbox import DeviceInbox
+
+    f = fns[tags[0]]
+    sizes = [int(np.prod(sh)) for _, sh in bench.resnet18_param_shapes()] * scale
+    w0 = [torch.empty(m, dtype=torch.float32, device=dev) for m in sizes]
+    for l, w in enumerate(w0):
+        ops.fill_synthetic_(w, 0x5EED0001 + l, 0xFFFFF, 5e-2)
+    inbox = DeviceInbox({f"k{l}": w for l, w in enumerate(w0)}, k_max=K, device=dev)
+    for p in range(K):
+        ops.fill_synthetic_(inbox.slab[p], 0x5EED0001, p, 1e-2)
+    offs = [inbox.layout[f"k{l}"][0] for l in range(len(sizes))]
+    views = [[inbox.slab[j, o:o + m] for o, m in zip(offs, sizes)] for j in range(K)]
+    if carve:
+        big = torch.empty(4 << 30, dtype=torch.float32, device=dev)
+        del big  # cached, not returned: the clones below are split from it
+    clones = [[v.clone() for v in row] for row in views]
+    ws = [w.clone() for w in w0]
+    st = torch.cuda.current_stream(dev).cuda_stream
+    ops._TABLES.clear()
+    rows = ops.aggregate_slab_rows_(ws, inbox.slab, list(range(K)), offs, "fedavg")
+    _, ch_off, ntiles = rows[5]
+    launches = {"rows (slab)": lambda: f[2](rows[0].data_ptr(), K, ntiles, rows[0].data_ptr() + ch_off, 0, 0.1, st)}
+    for name, src in (("chunks (clones)", clones), ("chunks (slab views)", views)):
+        ptrs = np.array([[src[j][l].data_ptr() for j in range(K)] for l in range(len(sizes))], dtype=np.uint64)
+        ops.aggregate_ptr_table_(ws, ptrs, "fedavg")
+        e = next(reversed(ops._TABLES.values()))
+        lst_off, S, segs_off, how = e[5][2]
+        assert how == "chunks" and e[1] == 0
+        b = e[0].data_ptr()
+        launches[name] = (lambda b=b, lst_off=lst_off, S=S, segs_off=segs_off:
+                          f[1](b + lst_off, S, b + segs_off, K, 0, 0.1, st))
+    torch.cuda.synchronize()
+    names = list(launches)
+    ms = {nm: [] for nm in names}
+    for r in range(reps):
+        for nm in (names if r % 2 == 0 else names[::-1]):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(2_000_000)
+            e0.record()
+            launches[nm]()
+            e1.record()
+            torch.cuda.synchronize()
+            ms[nm].append(e0.elapsed_time(e1))
+    report(f"rows vs clones K={K} x{scale} ({ntiles} tiles, build {tags[0]}{', clones carved' if carve else ''})", K,
+           sum(sizes), True, ms)
+    del inbox, ws, w0, clones, views
+    ops._TABLES.clear()
+    torch.cuda.empty_cache()
+    return True
+
+
 def state_dict_case(fns, tags, K, scale, reps, dev, place="alloc"):
     """ResNet-18's 62 shapes x scale as separately allocated tensors x K: the
     chunk list and segment table built once by the product's host code
@@ -215,6 +275,9 @@ def main():
     for case in cases:
         if case[0] == "delta":
             ok &= delta_case(fns, tags, int(case[1]), reps, dev)
+            continue
+        if case[0] == "rowsclone":
+            ok &= rows_vs_clones_case(fns, tags, int(case[1]), int(case[2]), reps, dev, *case[3:])
             continue
         if case[0] in ("sd", "rows"):
             fn = state_dict_case if case[0] == "sd" else rows_case
