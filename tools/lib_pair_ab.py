@@ -142,7 +142,6 @@ def rows_vs_clones_case(fns, tags, K, scale, reps, dev, carve=""):
     import bench
     from p2pdl_amd.node.inbox import DeviceInbox
 
-    f = fns[tags[0]]
     sizes = [int(np.prod(sh)) for _, sh in bench.resnet18_param_shapes()] * scale
     w0 = [torch.empty(m, dtype=torch.float32, device=dev) for m in sizes]
     for l, w in enumerate(w0):
@@ -161,16 +160,34 @@ def rows_vs_clones_case(fns, tags, K, scale, reps, dev, carve=""):
     ops._TABLES.clear()
     rows = ops.aggregate_slab_rows_(ws, inbox.slab, list(range(K)), offs, "fedavg")
     _, ch_off, ntiles = rows[5]
-    launches = {"rows (slab)": lambda: f[2](rows[0].data_ptr(), K, ntiles, rows[0].data_ptr() + ch_off, 0, 0.1, st)}
+    launches = {}
+    chunk_tables = {}
     for name, src in (("chunks (clones)", clones), ("chunks (slab views)", views)):
         ptrs = np.array([[src[j][l].data_ptr() for j in range(K)] for l in range(len(sizes))], dtype=np.uint64)
         ops.aggregate_ptr_table_(ws, ptrs, "fedavg")
         e = next(reversed(ops._TABLES.values()))
         lst_off, S, segs_off, how = e[5][2]
         assert how == "chunks" and e[1] == 0
-        b = e[0].data_ptr()
-        launches[name] = (lambda b=b, lst_off=lst_off, S=S, segs_off=segs_off:
-                          f[1](b + lst_off, S, b + segs_off, K, 0, 0.1, st))
+        chunk_tables[name] = (e, lst_off, S, segs_off)
+    same = True
+    for ti, t in enumerate(tags):
+        f = fns[t]
+        pre = f"{t} " if len(tags) > 1 else ""
+        launches[pre + "rows (slab)"] = (lambda f=f: f[2](rows[0].data_ptr(), K, ntiles, rows[0].data_ptr() + ch_off,
+                                                           0, 0.1, st))
+        for name, (e, lst_off, S, segs_off) in chunk_tables.items():
+            b = e[0].data_ptr()
+            launches[pre + name] = (lambda f=f, b=b, lst_off=lst_off, S=S, segs_off=segs_off:
+                                    f[1](b + lst_off, S, b + segs_off, K, 0, 0.1, st))
+        for w, a in zip(ws, w0):  # every build's chunk list over the clones from the same w: bit-compared
+            w.copy_(a)
+        launches[pre + "chunks (clones)"]()
+        torch.cuda.synchronize()
+        got = torch.cat(ws).cpu().numpy().view(np.uint32)
+        if ti == 0:
+            first = got
+        else:
+            same &= bool(np.array_equal(got, first))
     torch.cuda.synchronize()
     names = list(launches)
     ms = {nm: [] for nm in names}
@@ -183,12 +200,12 @@ def rows_vs_clones_case(fns, tags, K, scale, reps, dev, carve=""):
             e1.record()
             torch.cuda.synchronize()
             ms[nm].append(e0.elapsed_time(e1))
-    report(f"rows vs clones K={K} x{scale} ({ntiles} tiles, build {tags[0]}{', clones carved' if carve else ''})", K,
-           sum(sizes), True, ms)
+    report(f"rows vs clones K={K} x{scale} ({ntiles} tiles, builds {'/'.join(tags)}{', clones carved' if carve else ''})",
+           K, sum(sizes), same, ms)
     del inbox, ws, w0, clones, views
     ops._TABLES.clear()
     torch.cuda.empty_cache()
-    return True
+    return same
 
 
 def state_dict_case(fns, tags, K, scale, reps, dev, place="alloc"):
