@@ -3,9 +3,12 @@
 under rocprofv3 --pmc (round 6): per launch, the rows kernel over the slab,
 the chunk list over .clone()d dicts and over the slab's own views.  The
 chunk-kernel dispatches are told apart by the case's fixed order: one setup
-launch over the clones, one over the views, then per rep [clones, views]
-(even reps) or [views, clones] (odd).  Measurement tool, not product.
-usage: tlb_summary.py <rocprofv3 output dir> [out.json]"""
+launch over the clones, one over the views, (since the case compares builds)
+one bit-check launch over the clones per build, then per rep [clones, views]
+(even reps) or [views, clones] (odd).  SETUP: the chunk launches before the
+reps -- 3 for one build (2 for the tool as profiles/r06/tlb/tlb_p*.json ran
+it).  Measurement tool, not product.
+usage: tlb_summary.py <rocprofv3 output dir> [out.json] [SETUP=3]"""
 import collections
 import csv
 import glob
@@ -29,11 +32,12 @@ def main():
     rows, chunks = [], []
     for i in sorted(disp):
         (rows if "false, 2," in disp[i]["kernel"] else chunks).append(disp[i]["c"])
-    labels = ["clones", "views"]
-    for rep in range((len(chunks) - 2) // 2):
+    setup = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    labels = []
+    for rep in range((len(chunks) - setup) // 2):
         labels += ["clones", "views"] if rep % 2 == 0 else ["views", "clones"]
     groups = {"rows (slab)": rows[1:], "chunks (clones)": [], "chunks (slab views)": []}
-    for lab, c in zip(labels[2:], chunks[2:]):
+    for lab, c in zip(labels, chunks[setup:]):
         groups["chunks (clones)" if lab == "clones" else "chunks (slab views)"].append(c)
     out = {}
     for g, cs in groups.items():
