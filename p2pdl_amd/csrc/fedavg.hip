@@ -783,7 +783,7 @@ static bool use_queue(bool share, const int32_t* k_dev, int K) {
   return queue_mode<MODE>() && !share && !k_dev && K >= kQueueMinK && K <= kQueueMaxK;
 }
 constexpr int kQueueCaptured = 1024;
-static std::atomic<uint32_t> g_queue_next{0};
+static std::atomic<uint64_t> g_queue_next{0};  // 64-bit: i mod 3,072 never jumps at a wrap
 static std::atomic<uint32_t> g_queue_captured{0};
 // The counter pair of a queued launch on `st`, or -1: launch without the queue.
 static int queue_slot(hipStream_t st) {
@@ -793,7 +793,7 @@ static int queue_slot(hipStream_t st) {
     return c < static_cast<uint32_t>(kQueueCaptured) ? kQueueSlots - kQueueCaptured + static_cast<int>(c) : -1;
   }
   return static_cast<int>(g_queue_next.fetch_add(1, std::memory_order_relaxed) %
-                          static_cast<uint32_t>(kQueueSlots - kQueueCaptured));
+                          static_cast<uint64_t>(kQueueSlots - kQueueCaptured));
 }
 // The split kernel over ntiles tiles in mode MODE: the tile queue's
 // persistent grid of min(tiles, CUs) blocks when built with it (K from the
