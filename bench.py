@@ -753,7 +753,7 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
         # behind a spin so no host time falls between the events
         from p2pdl_amd.aggregator.model_state import model_state
 
-        _, ws_m, st_m = model_state(model)
+        keys_m, ws_m, st_m = model_state(model)
         launch = st_m.extra.get("launch") if st_m is not None else None
         kernel_path = (("split kernel over the slab rows as flat peers (ops._rows_entry)"
                         if launch[2][5][0] == "rows" else "VGPR segment kernel (+ split tiles when planned)")
@@ -772,6 +772,18 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
         gen_entry = next(reversed(ops._TABLES.values()))
         general_kernel_ms = kernel_only_ms(lambda: ops.relaunch(gen_entry, dev, len(keys), K, 0.1), steps, comp)
         general_route = gen_entry[5][2][3] if gen_entry[5][0] != "rows" and gen_entry[5][2] else "vgpr"
+        # the same route over the slab rows' own views (the landed bytes, one
+        # allocation): what the kernel reads there against the per-tensor
+        # allocations above is where the caller's allocator put the tensors
+        # (UTCL1 translation misses), not the kernel
+        import numpy as np
+
+        vptrs = np.array([[slab[j].data_ptr() + 4 * inbox.layout[k][0] for j in range(K)] for k in keys_m],
+                         dtype=np.uint64)
+        ops.aggregate_ptr_table_(ws_m, vptrs, "fedavg")
+        v_entry = next(reversed(ops._TABLES.values()))
+        views_route = v_entry[5][2][3] if v_entry[5][0] != "rows" and v_entry[5][2] else "vgpr"
+        views_kernel_ms = kernel_only_ms(lambda: ops.relaunch(v_entry, dev, len(keys), K, 0.1), steps, comp)
         fresh = []
         for _ in range(steps):
             ops._TABLES.clear()
@@ -820,7 +832,13 @@ def measure_dropin(c: Ctx, args, name, K, seed, steps, warmup, cpu_s):
             "route": general_route, "us_per_call": round(general_s * 1e6, 1),
             "us_per_call_new_table_every_call": round(general_fresh_s * 1e6, 1),
             "kernel_ms": round(general_kernel_ms, 4),
-            "frac_of_hbm_peak": round(4 * n * (K + 2) / (general_kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "frac_of_hbm_peak": round(4 * n * (K + 2) / (general_kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "same_route_over_slab_views": {
+                "route": views_route, "kernel_ms": round(views_kernel_ms, 4),
+                "frac_of_hbm_peak": round(4 * n * (K + 2) / (views_kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "what": "the general path's table built over the DeviceInbox slab rows' own views (one "
+                        "allocation) instead of per-tensor clones: the kernel's rate without the clones' "
+                        "address-translation misses"}},
         "reference_on_gpu": None if ref_s is None else {
             "us_per_call": round(ref_s * 1e6, 1), "speedup": round(ref_s / step_s, 1),
             "what": "the reference's aggregate_models loop (aggregation.py:15-38) as a node on this GPU runs "
